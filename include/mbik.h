@@ -1,0 +1,139 @@
+/*
+ * mbik.h -- C ABI of the MI355X-native batched many-bone IK solver.
+ *
+ * Drop-in boundary for the per-frame solve path of Ughuuu/many_bone_ik
+ * (snapshot 2024-08-07).  Each entry point names the reference interface it replaces:
+ *
+ *   mbik_plan_create   <- ManyBoneIK3D::_bone_list_changed()      src/many_bone_ik_3d.cpp:1011-1068
+ *                         (segmentation, heading weights, bone directions, Kusudama setup;
+ *                          IKBoneSegment3D::generate_default_segments ik_bone_segment_3d.cpp:352-427,
+ *                          IKBone3D::update_default_bone_direction_transform ik_bone_3d.cpp:57-93,
+ *                          IKLimitCone3D::update_tangent_handles ik_open_cone_3d.cpp:36-120,
+ *                          IKKusudama3D::set_axial_limits/_update_constraint ik_kusudama_3d.cpp:37-115)
+ *   mbik_solve         <- ManyBoneIK3D::_process_modification()   src/many_bone_ik_3d.cpp:645-694
+ *                         (the virtual SkeletonModifier3D hook, many_bone_ik_3d.h:90; preceded by
+ *                          _update_ik_bones_transform :91-102 and followed by
+ *                          _update_skeleton_bones_transform :104-116), for a batch of skeletons
+ *   mbik_solve_host    <- same, synchronous, host buffers
+ *   mbik_segment_solve <- IKBoneSegment3D::segment_solver()       src/ik_bone_segment_3d.cpp:210-225
+ *                         (one call = one segment_solver() of one segment subtree)
+ *   mbik_plan_destroy  <- ~ManyBoneIK3D / set_dirty() rebuild
+ *   mbik_last_error    <- ERR_FAIL_* messages (the reference prints and returns)
+ *
+ * Plain pointers and sizes only.  All float arrays are float32, row-major, one skeleton
+ * after another:
+ *   pose    [skel][bone][10]  quaternion x,y,z,w | position x,y,z | scale x,y,z
+ *                             (Skeleton3D bone pose; ik_bone_3d.cpp:161-179)
+ *   target  [skel][pin][12]   basis rows r0,r1,r2 | origin, in skeleton space
+ *                             (IKEffector3D::target_relative_to_skeleton_origin, ik_effector_3d.cpp:77-84)
+ *   cones   [skel][constraint][max_cones][4]  centre x,y,z | radius (kusudama_open_cones)
+ *   twist   [skel][constraint][2]             from, range (joint_twist)
+ *
+ * Threading: a plan is not thread-safe; distinct plans may be used concurrently on
+ * distinct streams.  mbik_solve is asynchronous on the given HIP stream.
+ * Errors: 0 on success, a negative MBIK_E* code otherwise; mbik_last_error() explains.
+ * Non-finite output bases become identity rotations, as ik_bone_3d.cpp:174-176 does.
+ */
+#ifndef MBIK_H
+#define MBIK_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MBIK_OK 0
+#define MBIK_EINVAL (-1)
+#define MBIK_ENOMEM (-2)
+#define MBIK_EHIP (-3)
+#define MBIK_EUNSUPPORTED (-4)
+#define MBIK_ENODEV (-5)
+
+#define MBIK_ABI_VERSION 1
+
+typedef struct mbik_plan mbik_plan;
+
+/* == IKEffectorTemplate3D (src/ik_effector_template_3d.h:40-47). */
+typedef struct mbik_pin {
+	int32_t bone;                      /* skeleton bone index (template name) */
+	float weight;                      /* reference default 0.0 */
+	float direction_priorities[3];     /* reference default (0.2, 0, 0.2) */
+	float motion_propagation_factor;   /* reference default 1.0, clamped to [0,1] */
+} mbik_pin;
+
+/* == one ManyBoneIK3D "constraints/<i>" entry (many_bone_ik_3d.cpp:1037-1067). */
+typedef struct mbik_constraint {
+	int32_t bone;                      /* constraint_names[i] resolved to a bone index */
+	int32_t cone_count;                /* kusudama_open_cone_count[i] */
+} mbik_constraint;
+
+typedef struct mbik_skeleton_desc {
+	int32_t bone_count;
+	const int32_t *parents;            /* [bone_count]; -1 = parentless */
+	int32_t pin_count;
+	const mbik_pin *pins;
+	int32_t constraint_count;
+	const mbik_constraint *constraints;
+	int32_t max_cones;                 /* stride of the cones array */
+} mbik_skeleton_desc;
+
+/* ManyBoneIK3D solver properties (many_bone_ik_3d.h:49-68). */
+typedef struct mbik_config {
+	int32_t iterations_per_frame;      /* reference default 15 */
+	float default_damp;                /* radians; reference default deg_to_rad(5) */
+	int32_t constraint_mode;           /* reference default false */
+	int32_t stabilization_passes;      /* reference default 0 */
+	int32_t bone_damp_count;           /* ManyBoneIK3D::bone_damp, usually empty */
+	const float *bone_damp;
+} mbik_config;
+
+typedef struct mbik_plan_info {
+	int32_t abi_version;
+	int32_t skeleton_count;
+	int32_t bone_count;
+	int32_t pin_count;
+	int32_t segment_count;
+	int32_t level_count;               /* sibling-segment levels solved concurrently */
+	int32_t lanes_per_skeleton;
+	int32_t skeletons_per_block;
+	int32_t max_headings;
+	int32_t device;
+	int64_t device_bytes;              /* per-skeleton plan tables resident in HBM */
+	double algorithmic_bytes_per_skeleton; /* pose in/out + targets + plan tables read once */
+} mbik_plan_info;
+
+/* Builds the per-topology tables and the per-skeleton setup data for skeletons
+ * [0, n_skeletons) from their setup poses, uploads them to `device`.  cones/twist may be
+ * NULL when constraint_count == 0. */
+int32_t mbik_plan_create(const mbik_skeleton_desc *desc, const mbik_config *config, int32_t n_skeletons,
+		const float *setup_pose, const float *cones, const float *twist, int32_t device, mbik_plan **out_plan);
+void mbik_plan_destroy(mbik_plan *plan);
+int32_t mbik_plan_get_info(const mbik_plan *plan, mbik_plan_info *out);
+/* Launch-shape override (0 = automatic).  lanes_per_skeleton must be a power of two <= 64. */
+int32_t mbik_plan_set_launch(mbik_plan *plan, int32_t lanes_per_skeleton);
+
+/* One frame for skeletons [first, first+count): device pointers (hipMalloc'd, on the
+ * plan's device), asynchronous on hip_stream (NULL = default stream).  pose_in, targets
+ * and pose_out are indexed from skeleton `first`. */
+int32_t mbik_solve(mbik_plan *plan, int32_t first, int32_t count, const float *pose_in, const float *targets,
+		float *pose_out, void *hip_stream);
+/* Same with host buffers; synchronous (copies in, solves, copies out). */
+int32_t mbik_solve_host(mbik_plan *plan, int32_t first, int32_t count, const float *pose_in, const float *targets,
+		float *pose_out);
+/* Runs IKBoneSegment3D::segment_solver() once on `segment` (index in post-order segment
+ * numbering of mbik_plan_segment_table) for every skeleton in [first, first+count), updating
+ * pose_inout in place (device pointers).  No pose write-back conversion is skipped: the
+ * output is the Skeleton3D pose of every IK bone after that call. */
+int32_t mbik_segment_solve(mbik_plan *plan, int32_t segment, int32_t first, int32_t count, float *pose_inout,
+		const float *targets, void *hip_stream);
+/* Segment table: for each segment, its root bone, tip bone and parent segment (-1). */
+int32_t mbik_plan_segment_table(const mbik_plan *plan, int32_t *root_bone, int32_t *tip_bone, int32_t *parent_segment,
+		int32_t capacity);
+
+const char *mbik_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MBIK_H */

@@ -1,0 +1,102 @@
+"""ctypes bindings of the C ABI (include/mbik.h) exported by libmbik.so.
+
+The product path always goes through this library: there is no CPU fallback.  If the
+in-tree libmbik.so is missing the import of any solver entry point fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmbik.so")
+
+MBIK_OK = 0
+MBIK_EINVAL = -1
+MBIK_ENOMEM = -2
+MBIK_EHIP = -3
+MBIK_EUNSUPPORTED = -4
+MBIK_ENODEV = -5
+
+EXPORTED_SYMBOLS = (
+    "mbik_plan_create", "mbik_plan_destroy", "mbik_plan_get_info", "mbik_plan_set_launch",
+    "mbik_solve", "mbik_solve_host", "mbik_segment_solve", "mbik_plan_segment_table", "mbik_last_error",
+)
+
+
+class MbikPin(C.Structure):
+    _fields_ = [("bone", C.c_int32), ("weight", C.c_float), ("direction_priorities", C.c_float * 3),
+                ("motion_propagation_factor", C.c_float)]
+
+
+class MbikConstraint(C.Structure):
+    _fields_ = [("bone", C.c_int32), ("cone_count", C.c_int32)]
+
+
+class MbikSkeletonDesc(C.Structure):
+    _fields_ = [("bone_count", C.c_int32), ("parents", C.POINTER(C.c_int32)),
+                ("pin_count", C.c_int32), ("pins", C.POINTER(MbikPin)),
+                ("constraint_count", C.c_int32), ("constraints", C.POINTER(MbikConstraint)),
+                ("max_cones", C.c_int32)]
+
+
+class MbikConfig(C.Structure):
+    _fields_ = [("iterations_per_frame", C.c_int32), ("default_damp", C.c_float),
+                ("constraint_mode", C.c_int32), ("stabilization_passes", C.c_int32),
+                ("bone_damp_count", C.c_int32), ("bone_damp", C.POINTER(C.c_float))]
+
+
+class MbikPlanInfo(C.Structure):
+    _fields_ = [("abi_version", C.c_int32), ("skeleton_count", C.c_int32), ("bone_count", C.c_int32),
+                ("pin_count", C.c_int32), ("segment_count", C.c_int32), ("level_count", C.c_int32),
+                ("lanes_per_skeleton", C.c_int32), ("skeletons_per_block", C.c_int32),
+                ("max_headings", C.c_int32), ("device", C.c_int32), ("device_bytes", C.c_int64),
+                ("algorithmic_bytes_per_skeleton", C.c_double)]
+
+
+class MbikError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"mbik error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def load():
+    """Load the in-tree libmbik.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is missing: build it with `python -m many_bone_ik_amd.build` "
+                          "(the HIP path has no CPU fallback)")
+    L = C.CDLL(LIB_PATH)
+    vp = C.c_void_p
+    L.mbik_plan_create.argtypes = [C.POINTER(MbikSkeletonDesc), C.POINTER(MbikConfig), C.c_int32, vp, vp, vp, C.c_int32,
+                                   C.POINTER(vp)]
+    L.mbik_plan_create.restype = C.c_int32
+    L.mbik_plan_destroy.argtypes = [vp]
+    L.mbik_plan_destroy.restype = None
+    L.mbik_plan_get_info.argtypes = [vp, C.POINTER(MbikPlanInfo)]
+    L.mbik_plan_get_info.restype = C.c_int32
+    L.mbik_plan_set_launch.argtypes = [vp, C.c_int32]
+    L.mbik_plan_set_launch.restype = C.c_int32
+    L.mbik_solve.argtypes = [vp, C.c_int32, C.c_int32, vp, vp, vp, vp]
+    L.mbik_solve.restype = C.c_int32
+    L.mbik_solve_host.argtypes = [vp, C.c_int32, C.c_int32, vp, vp, vp]
+    L.mbik_solve_host.restype = C.c_int32
+    L.mbik_segment_solve.argtypes = [vp, C.c_int32, C.c_int32, C.c_int32, vp, vp, vp]
+    L.mbik_segment_solve.restype = C.c_int32
+    L.mbik_plan_segment_table.argtypes = [vp, vp, vp, vp, C.c_int32]
+    L.mbik_plan_segment_table.restype = C.c_int32
+    L.mbik_last_error.argtypes = []
+    L.mbik_last_error.restype = C.c_char_p
+    _lib = L
+    return L
+
+
+def check(rc: int) -> int:
+    if rc < 0:
+        raise MbikError(rc, load().mbik_last_error().decode(errors="replace"))
+    return rc

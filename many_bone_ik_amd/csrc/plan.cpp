@@ -1,0 +1,604 @@
+// Host plan builder: a flat restatement of ManyBoneIK3D::_bone_list_changed
+// (src/many_bone_ik_3d.cpp:1011-1068) and everything it calls, producing the tables
+// the gfx950 solve kernel reads.  No object graph: segment structure, effector lists and
+// heading weights are computed once per topology; bone-direction and Kusudama frames once
+// per skeleton (they depend on the setup pose).
+#include "plan.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <functional>
+
+#include "gd_math.h"
+
+namespace mbik {
+
+using namespace gd;
+
+// ---------------------------------------------------------------------------------------
+// Topology
+// ---------------------------------------------------------------------------------------
+std::string build_topology(const mbik_skeleton_desc &desc, const mbik_config &cfg, HostPlan &p) {
+	const int B = desc.bone_count;
+	if (B <= 0 || !desc.parents) return "bone_count must be > 0 and parents non-null";
+	if (desc.pin_count < 0 || (desc.pin_count > 0 && !desc.pins)) return "invalid pins";
+	if (desc.constraint_count < 0 || (desc.constraint_count > 0 && !desc.constraints)) return "invalid constraints";
+	if (cfg.iterations_per_frame < 0) return "iterations_per_frame must be >= 0";
+	p.B = B;
+	p.P = desc.pin_count;
+	p.max_cones = std::max(1, desc.max_cones);
+	p.iterations = cfg.iterations_per_frame;
+	p.constraint_mode = cfg.constraint_mode;
+	p.stabilization_passes = cfg.stabilization_passes;
+	p.parents.assign(desc.parents, desc.parents + B);
+	for (int b = 0; b < B; b++)
+		if (p.parents[b] < -1 || p.parents[b] >= B || p.parents[b] == b) return "parents out of range";
+	// Skeleton3D::get_bone_children: ascending bone index.
+	std::vector<std::vector<int>> kids(B);
+	for (int b = 0; b < B; b++)
+		if (p.parents[b] >= 0) kids[p.parents[b]].push_back(b);
+	// cycle check + depth
+	p.bone_depth.assign(B, -1);
+	std::function<int(int, int)> depth_of = [&](int b, int guard) -> int {
+		if (guard > B) return -1000000;
+		if (p.bone_depth[b] >= 0) return p.bone_depth[b];
+		int d = p.parents[b] < 0 ? 0 : depth_of(p.parents[b], guard + 1) + 1;
+		p.bone_depth[b] = d;
+		return d;
+	};
+	for (int b = 0; b < B; b++)
+		if (depth_of(b, 0) < 0) return "parents contain a cycle";
+	// IKBone3D ctor: first matching IKEffectorTemplate3D (ik_bone_3d.cpp:209-222).
+	p.bone_pin.assign(B, -1);
+	for (int i = desc.pin_count; i-- > 0;) {
+		int b = desc.pins[i].bone;
+		if (b < 0 || b >= B) return "pin bone out of range";
+		p.bone_pin[b] = i;
+	}
+	p.eff_bone.resize(p.P);
+	p.eff_prio.resize(3 * p.P);
+	for (int i = 0; i < p.P; i++) {
+		p.eff_bone[i] = desc.pins[i].bone;
+		for (int a = 0; a < 3; a++) p.eff_prio[3 * i + a] = desc.pins[i].direction_priorities[a];
+	}
+	auto mpf = [&](int pin) -> float { // IKEffector3D::set_motion_propagation_factor clamps
+		double v = desc.pins[pin].motion_propagation_factor;
+		return (float)(v < 0.0 ? 0.0 : (v > 1.0 ? 1.0 : v));
+	};
+
+	// IKBoneSegment3D::generate_default_segments (ik_bone_segment_3d.cpp:352-427).
+	struct Seg {
+		int root, tip = -1, parent;
+		std::vector<int> kept, bones;
+		bool pinned_desc = false;
+	};
+	std::vector<Seg> segs;
+	p.bone_ik_parent.assign(B, -1);
+	std::function<void(int)> gen = [&](int si) {
+		int cur = segs[si].root;
+		for (;;) {
+			const auto &ch = kids[cur];
+			if (ch.empty() || ch.size() > 1 || p.bone_pin[cur] >= 0) {
+				segs[si].tip = cur;
+				for (int c : ch) {
+					int ci = (int)segs.size();
+					segs.push_back(Seg{c, -1, si});
+					p.bone_ik_parent[c] = cur; // root->set_parent(p_parent->get_tip()) :259-262
+					gen(ci);
+					if (segs[ci].pinned_desc) {
+						segs[si].pinned_desc = true;
+						segs[si].kept.push_back(ci);
+					}
+				}
+				break;
+			}
+			int nx = ch[0];
+			p.bone_ik_parent[nx] = cur; // _create_next_bone :401-407
+			cur = nx;
+		}
+		Seg &g = segs[si];
+		g.tip = cur;
+		if (p.bone_pin[g.tip] >= 0) g.pinned_desc = true;
+		for (int b = g.tip; b >= 0; b = p.bone_ik_parent[b]) {
+			g.bones.push_back(b);
+			if (b == g.root) break;
+		}
+	};
+	std::vector<int> root_segs;
+	for (int r = 0; r < B; r++) {
+		if (p.parents[r] >= 0) continue;
+		root_segs.push_back((int)segs.size());
+		segs.push_back(Seg{r, -1, -1});
+		gen(root_segs.back());
+	}
+	if (root_segs.empty()) return "skeleton has no parentless bone";
+
+	// Kept segments in solve (post-order) numbering; bone_list per create_bone_list(true).
+	std::vector<int> order; // old ids in post-order
+	std::function<void(int)> post = [&](int si) {
+		for (int c : segs[si].kept) post(c);
+		order.push_back(si);
+	};
+	std::vector<int> new_id(segs.size(), -1);
+	for (int r : root_segs) post(r);
+	for (size_t i = 0; i < order.size(); i++) new_id[order[i]] = (int)i;
+	p.NS = (int)order.size();
+	p.seg_root.resize(p.NS);
+	p.seg_tip.resize(p.NS);
+	p.seg_parent.resize(p.NS);
+	p.seg_children.assign(p.NS, {});
+	p.seg_flags.assign(p.NS, 0);
+	p.seg_bone_off.assign(1, 0);
+	p.bone_list.clear();
+	for (int i = 0; i < p.NS; i++) {
+		const Seg &g = segs[order[i]];
+		p.seg_root[i] = g.root;
+		p.seg_tip[i] = g.tip;
+		p.seg_parent[i] = g.parent >= 0 ? new_id[g.parent] : -1;
+		for (int c : g.kept) p.seg_children[i].push_back(new_id[c]);
+		if (g.parent < 0) p.seg_flags[i] |= SF_TRANSLATE;
+		for (int b : g.bones) {
+			p.seg_bones.push_back(b);
+			p.bone_list.push_back(b);
+		}
+		p.seg_bone_off.push_back((int)p.seg_bones.size());
+	}
+	for (int r : root_segs) p.roots.push_back(new_id[r]);
+
+	// Pose-node parents: ik_origin is re-instantiated per root, so only the last root keeps
+	// one (many_bone_ik_3d.cpp:1022-1023; the released origin's cleanup() detaches its child).
+	p.bone_pose_parent.assign(B, POSE_PARENT_NONE);
+	for (int b = 0; b < B; b++) p.bone_pose_parent[b] = p.bone_ik_parent[b];
+	for (size_t i = 0; i < root_segs.size(); i++)
+		p.bone_pose_parent[segs[root_segs[i]].root] = (i + 1 == root_segs.size()) ? POSE_PARENT_ORIGIN : POSE_PARENT_NONE;
+
+	// update_pinned_list (:74-88) and recursive_create_penalty_array (:309-343).
+	std::vector<std::vector<int>> effl(p.NS);
+	for (int i = 0; i < p.NS; i++) { // post-order: children done first
+		int tip = p.seg_tip[i];
+		bool pinned = p.bone_pin[tip] >= 0;
+		if (pinned) effl[i].push_back(p.bone_pin[tip]);
+		double f = pinned ? (double)mpf(p.bone_pin[tip]) : 1.0;
+		if (f > 0.0)
+			for (int c : p.seg_children[i]) effl[i].insert(effl[i].end(), effl[c].begin(), effl[c].end());
+	}
+	std::function<void(int, std::vector<double> &, double)> penalty = [&](int si, std::vector<double> &out, double falloff) {
+		if (falloff <= 0.0) return;
+		double current = 1.0;
+		int tip = p.seg_tip[si];
+		if (p.bone_pin[tip] >= 0) {
+			const mbik_pin &pin = desc.pins[p.bone_pin[tip]];
+			double weight = pin.weight;
+			out.push_back(weight * falloff);
+			const float *pr = pin.direction_priorities;
+			float mx = std::max(std::max(pr[0], pr[1]), pr[2]);
+			double mpw = mx;
+			mpw = mpw == 0.0 ? 1.0 : mpw;
+			for (int a = 0; a < 3; a++) {
+				double pri = pr[a];
+				if (pri > 0.0) {
+					double sub = weight * (pri / mpw) * falloff;
+					out.push_back(sub);
+					out.push_back(sub);
+				}
+			}
+			current = mpf(p.bone_pin[tip]);
+		}
+		for (int c : p.seg_children[si]) penalty(c, out, falloff * current);
+	};
+	auto nheads = [&](int pin) {
+		int n = 1;
+		for (int a = 0; a < 3; a++)
+			if (desc.pins[pin].direction_priorities[a] > 0.0) n += 2;
+		return n;
+	};
+	p.seg_eff_off.assign(1, 0);
+	p.seg_hw_off.assign(p.NS, 0);
+	p.seg_nh.assign(p.NS, 0);
+	p.max_headings = 0;
+	for (int i = 0; i < p.NS; i++) {
+		std::vector<double> w;
+		penalty(i, w, 1.0);
+		int h = 0;
+		for (int e : effl[i]) {
+			p.seg_effs.push_back(e);
+			p.seg_eff_hoff.push_back(h);
+			h += nheads(e);
+		}
+		if ((size_t)h != w.size()) return "heading count mismatch between effector list and penalty array";
+		p.seg_eff_off.push_back((int)p.seg_effs.size());
+		p.seg_hw_off[i] = (int)p.seg_hw.size();
+		p.seg_hw.insert(p.seg_hw.end(), w.begin(), w.end());
+		p.seg_nh[i] = h;
+		p.max_headings = std::max(p.max_headings, h);
+	}
+	// Damping per (segment, bone): _qcp_solver (:227-240); the root segment uses PI (:217-222).
+	p.seg_cos_half_damp.clear();
+	for (int i = 0; i < p.NS; i++) {
+		for (int k = p.seg_bone_off[i]; k < p.seg_bone_off[i + 1]; k++) {
+			int b = p.seg_bones[k];
+			float d;
+			if (p.seg_flags[i] & SF_TRANSLATE) {
+				d = (float)gd::PI;
+			} else {
+				float def = cfg.default_damp;
+				d = def;
+				if (b < cfg.bone_damp_count && cfg.bone_damp) d = cfg.bone_damp[b];
+				if (def < d) d = def;
+			}
+			double dampening = (double)(float)(double)d; // float -> double -> float p_dampening -> double
+			p.seg_cos_half_damp.push_back(std::cos(dampening / 2.0));
+		}
+	}
+	// Effector paths from the skeleton root, pinned IK children per bone.
+	p.eff_parent_bone.assign(p.P, -1);
+	p.eff_path_off.assign(1, 0);
+	for (int e = 0; e < p.P; e++) {
+		int b = p.eff_bone[e];
+		p.eff_parent_bone[e] = p.bone_ik_parent[b];
+		std::vector<int> path;
+		for (int x = b; x >= 0; x = p.parents[x]) path.push_back(x);
+		std::reverse(path.begin(), path.end());
+		p.eff_path.insert(p.eff_path.end(), path.begin(), path.end());
+		p.eff_path_off.push_back((int)p.eff_path.size());
+	}
+	p.bone_flags.assign(B, 0);
+	for (int b : p.bone_list) p.bone_flags[b] |= BF_IN_LIST;
+	for (int b = 0; b < B; b++)
+		if (p.bone_pin[b] >= 0 && (p.bone_flags[b] & BF_IN_LIST)) p.bone_flags[b] |= BF_PINNED;
+	p.bone_child_eff_off.assign(1, 0);
+	for (int b = 0; b < B; b++) {
+		for (int c : kids[b])
+			if ((p.bone_flags[c] & BF_PINNED) && p.bone_ik_parent[c] == b) p.bone_child_effs.push_back(p.bone_pin[c]);
+		p.bone_child_eff_off.push_back((int)p.bone_child_effs.size());
+	}
+	// Constraint slots: named constraints whose bone is in the bone list (:1037-1067).
+	p.bone_cons.assign(B, -1);
+	p.cons_bone.clear();
+	p.cons_ncones.clear();
+	p.cons_order.clear();
+	p.cons_order_slot.clear();
+	p.cons_order_ncones.clear();
+	p.desc_constraint_count = desc.constraint_count;
+	for (int c = 0; c < desc.constraint_count; c++) {
+		int b = desc.constraints[c].bone;
+		if (b < 0 || b >= B) return "constraint bone out of range";
+		if (desc.constraints[c].cone_count < 0 || desc.constraints[c].cone_count > desc.max_cones)
+			return "constraint cone_count exceeds max_cones";
+		if (!(p.bone_flags[b] & BF_IN_LIST)) continue;
+		if (p.bone_cons[b] < 0) {
+			p.bone_cons[b] = (int)p.cons_bone.size();
+			p.cons_bone.push_back(b);
+			p.cons_ncones.push_back(desc.constraints[c].cone_count);
+		} else {
+			p.cons_ncones[p.bone_cons[b]] = desc.constraints[c].cone_count; // later constraint replaces
+		}
+		p.cons_order.push_back(c);
+		p.cons_order_slot.push_back(p.bone_cons[b]);
+		p.cons_order_ncones.push_back(desc.constraints[c].cone_count);
+		if (p.bone_ik_parent[b] >= 0) p.bone_flags[b] |= BF_ORIENT | BF_AXIAL;
+	}
+	p.NC = (int)p.cons_bone.size();
+	// Segment heights (for sibling-level scheduling) and Euler-tour ranges.
+	p.seg_height.assign(p.NS, 0);
+	for (int i = 0; i < p.NS; i++)
+		for (int c : p.seg_children[i]) p.seg_height[i] = std::max(p.seg_height[i], p.seg_height[c] + 1);
+	p.seg_tin.assign(p.NS, 0);
+	p.seg_tout.assign(p.NS, 0);
+	for (int i = 0; i < p.NS; i++) { // post-order: subtree of i = [tin, i]
+		int lo = i;
+		for (int c : p.seg_children[i]) lo = std::min(lo, p.seg_tin[c]);
+		p.seg_tin[i] = lo;
+		p.seg_tout[i] = i;
+	}
+	return "";
+}
+
+// ---------------------------------------------------------------------------------------
+// IKLimitCone3D / IKRay3D setup geometry (ik_open_cone_3d.cpp:36-120, ik_ray_3d.cpp:64-166)
+// ---------------------------------------------------------------------------------------
+namespace {
+struct Cone {
+	V3 cp = {0, 1, 0};
+	double radius = 0, rcos = 0;
+	V3 t1 = {0, 0, 0}, t2 = {0, 0, 0};
+	double tr = 0, trcos = 0;
+};
+struct Ray {
+	V3 p1, p2;
+};
+void elongate(Ray &r, float amt) {
+	V3 mid = (r.p1 + r.p2) * 0.5f;
+	V3 h1 = r.p1 - mid, h2 = r.p2 - mid;
+	V3 a1 = normalized(h1) * amt, a2 = normalized(h2) * amt;
+	r.p1 = h1 + a1 + mid;
+	r.p2 = h2 + a2 + mid;
+}
+V3 intersects_plane(const Ray &r, V3 ta, V3 tb, V3 tc) {
+	V3 tta = ta - r.p1, ttb = tb - r.p1, ttc = tc - r.p1;
+	V3 u = ttb - tta, v = ttc - tta;
+	V3 dir = r.p2 - r.p1;
+	V3 n = normalized(cross(u, v));
+	V3 w0 = v3(0, 0, 0) - tta;
+	float a = -(dot(n, w0));
+	float b = dot(n, dir);
+	float rr = a / b;
+	return dir * rr + r.p1;
+}
+void intersects_sphere(const Ray &r, float radius, V3 &S1, V3 &S2) {
+	V3 rp1 = r.p1 - v3(0, 0, 0), rp2 = r.p2 - v3(0, 0, 0);
+	V3 e = normalized(rp2 - rp1);
+	V3 h = v3(0, 0, 0) - rp1;
+	float lf = dot(e, h);
+	float radpow = radius * radius;
+	float hdh = length_sq(h);
+	float lfpow = lf * lf;
+	float s = radpow - hdh + lfpow;
+	if (s >= 0.0f) {
+		s = sqrtf(s);
+		if (lf < s) {
+			if (lf + s >= 0) s = -s;
+		}
+		S1 = e * (lf - s) + rp1;
+		S2 = e * (lf + s) + rp1;
+	}
+	S1 = S1 + v3(0, 0, 0);
+	S2 = S2 + v3(0, 0, 0);
+}
+V3 get_orthogonal(V3 p) {
+	float threshold = length(p) * 0.6f;
+	if (threshold > 0.f) {
+		if (fabsf(p.x) <= threshold) {
+			float inv = 1.f / sqrtf(p.y * p.y + p.z * p.z);
+			return v3(0.f, inv * p.z, -inv * p.y);
+		} else if (fabsf(p.y) <= threshold) {
+			float inv = 1.f / sqrtf(p.x * p.x + p.z * p.z);
+			return v3(-inv * p.z, 0.f, inv * p.x);
+		}
+		float inv = 1.f / sqrtf(p.x * p.x + p.y * p.y);
+		return v3(inv * p.y, -inv * p.x, 0.f);
+	}
+	return v3(0, 0, 0);
+}
+void set_control_point(Cone &c, V3 v) {
+	if (is_zero_approx(length_sq(v))) c.cp = v3(0, 1, 0);
+	else c.cp = normalized(v);
+}
+void update_tangent_handles(Cone &c, const Cone *next) {
+	if (!next) return;
+	double radA = c.radius, radB = next->radius;
+	V3 A = c.cp, Bv = next->cp;
+	V3 arc_normal = normalized(cross(A, Bv));
+	double tRadius = (gd::PI - (radA + radB)) / 2;
+	double bA = radA + tRadius, bB = radB + tRadius;
+	V3 scaledAxisA = A * (float)std::cos(bA);
+	V3 planeDir1A = xform(axis_angle_sq(arc_normal, (float)bA), A);
+	V3 planeDir2A = xform(axis_angle_sq(A, (float)(gd::PI / 2)), planeDir1A);
+	V3 scaledAxisB = Bv * (float)std::cos(bB);
+	V3 planeDir1B = xform(axis_angle_sq(arc_normal, (float)bB), Bv);
+	V3 planeDir2B = xform(axis_angle_sq(Bv, (float)(gd::PI / 2)), planeDir1B);
+	Ray r1B{planeDir1B, scaledAxisB}, r2B{planeDir1B, planeDir2B};
+	elongate(r1B, 99);
+	elongate(r2B, 99);
+	V3 i1 = intersects_plane(r1B, scaledAxisA, planeDir1A, planeDir2A);
+	V3 i2 = intersects_plane(r2B, scaledAxisA, planeDir1A, planeDir2A);
+	Ray ir{i1, i2};
+	elongate(ir, 99);
+	V3 S1 = v3(0, 0, 0), S2 = v3(0, 0, 0);
+	intersects_sphere(ir, 1.0f, S1, S2);
+	c.t1 = normalized(S1);
+	c.t2 = normalized(S2);
+	c.tr = tRadius;
+	c.trcos = std::cos(tRadius);
+	if (is_zero_approx(length_sq(c.t1))) c.t1 = normalized(get_orthogonal(c.cp));
+	if (is_zero_approx(length_sq(c.t2))) c.t2 = normalized(get_orthogonal(c.t1 * -1.0f));
+}
+void update_tangent_radii(std::vector<Cone> &cs) {
+	for (size_t i = 0; i < cs.size(); i++) update_tangent_handles(cs[i], i + 1 < cs.size() ? &cs[i + 1] : nullptr);
+}
+} // namespace
+
+// ---------------------------------------------------------------------------------------
+// Per-skeleton setup data
+// ---------------------------------------------------------------------------------------
+std::string build_skeletons(HostPlan &p, int32_t n, const float *setup_pose, const float *cones, const float *twist,
+		int32_t max_cones_in) {
+	const int B = p.B, NC = p.NC;
+	if (n <= 0 || !setup_pose) return "n_skeletons must be > 0 and setup_pose non-null";
+	if (NC > 0 && (!cones || !twist)) return "cones/twist required when constraints exist";
+	p.N = n;
+	const size_t N = (size_t)n;
+	p.D.assign((size_t)B * 9 * N, 0.0f);
+	const int cfs = p.cf_stride(), cds = p.cd_stride();
+	p.CF.assign((size_t)NC * cfs * N, 0.0f);
+	p.CD.assign((size_t)NC * cds * N, 0.0);
+	// topological order (parents first)
+	std::vector<int> topo;
+	{
+		std::vector<std::vector<int>> kids(B);
+		for (int b = 0; b < B; b++)
+			if (p.parents[b] >= 0) kids[p.parents[b]].push_back(b);
+		std::vector<int> stack;
+		for (int b = B; b-- > 0;)
+			if (p.parents[b] < 0) stack.push_back(b);
+		while (!stack.empty()) {
+			int b = stack.back();
+			stack.pop_back();
+			topo.push_back(b);
+			for (size_t k = kids[b].size(); k-- > 0;) stack.push_back(kids[b][k]);
+		}
+	}
+	// Constraint contributions per slot (all named constraints on that bone, in order).
+	std::vector<X3> L(B), G(B);
+	std::vector<B3> Dm(B);
+	for (int s = 0; s < n; s++) {
+		const float *pose = setup_pose + (size_t)s * B * 10;
+		for (int b = 0; b < B; b++) L[b] = (p.bone_flags[b] & BF_IN_LIST) ? pose_to_xform(pose + 10 * b) : xid();
+		for (int b : topo) {
+			int pp = p.bone_pose_parent[b];
+			if (pp >= 0) G[b] = G[pp] * L[b];
+			else if (pp == POSE_PARENT_ORIGIN) G[b] = xid() * L[b];
+			else G[b] = L[b];
+		}
+		for (int b = 0; b < B; b++) Dm[b] = bid();
+		// IKBone3D::update_default_bone_direction_transform (ik_bone_3d.cpp:57-93), bone_list order.
+		for (int b : p.bone_list) {
+			V3 cc = v3(0, 0, 0);
+			int count = 0;
+			for (int c = 0; c < B; c++)
+				if (p.bone_ik_parent[c] == b) {
+					cc = cc + G[c].o;
+					count++;
+				}
+			cc = divs(cc, (float)count); // count == 0 -> 0/0 (NaN), as the reference
+			cc = cc - G[b].o;
+			if (is_zero_approx(length_sq(cc))) {
+				int par = p.bone_ik_parent[b];
+				cc = par >= 0 ? col(G[par].b * Dm[par], 1) : col(G[b].b * Dm[b], 1);
+			}
+			if (!is_zero_approx(length_sq(cc)) && count > 0) {
+				cc = normalized(cc);
+				V3 bd = normalized(col(G[b].b * Dm[b], 1));
+				B3 P = G[b].b;
+				Dm[b] = ((inverse(P) * from_quat(arc(cc, bd))) * P) * Dm[b];
+			}
+		}
+		for (int b = 0; b < B; b++)
+			for (int f = 0; f < 9; f++) p.D[((size_t)b * 9 + f) * N + s] = Dm[b].r[f / 3][f % 3];
+		if (NC == 0) continue;
+		// Kusudama setup, in the constraint order of the description (:1037-1067).
+		std::vector<B3> T(NC, bid());
+		std::vector<std::vector<Cone>> kc(NC);
+		std::vector<Q> tcr(NC, qid());
+		std::vector<float> thc(NC, 0.0f);
+		for (int c = 0; c < (int)p.cons_order.size(); c++) {
+			int ci = p.cons_order[c];        // index into the description's constraint array
+			int slot = p.cons_order_slot[c];
+			int b = p.cons_bone[slot];
+			int ncones = p.cons_order_ncones[c];
+			const float *cn = cones + ((size_t)s * p.desc_constraint_count + ci) * max_cones_in * 4;
+			const float *tw = twist + ((size_t)s * p.desc_constraint_count + ci) * 2;
+			std::vector<Cone> cs;
+			for (int k = 0; k < ncones; k++) {
+				Cone cone;
+				double rad = cn[4 * k + 3];
+				cone.radius = 1.0e-38 > rad ? 1.0e-38 : rad;
+				cone.rcos = std::cos(cone.radius);
+				set_control_point(cone, normalized(v3(cn[4 * k], cn[4 * k + 1], cn[4 * k + 2])));
+				cs.push_back(cone);
+				update_tangent_radii(cs);
+			}
+			// set_axial_limits (ik_kusudama_3d.cpp:103-115)
+			float min_angle = tw[0], range = tw[1];
+			V3 y_axis = v3(0, 1, 0), z_axis = v3(0, 0, 1);
+			Q twist_min_rot = axis_angle_sq(y_axis, min_angle);
+			V3 twist_min_vec = normalized(xform(twist_min_rot, z_axis));
+			V3 twist_center_vec = normalized(xform(twist_min_rot, twist_min_vec));
+			tcr[slot] = arc(z_axis, twist_center_vec);
+			thc[slot] = cos_f(range / 4.0f);
+			// _update_constraint(twist node) (ik_kusudama_3d.cpp:37-89)
+			V3 sum = v3(0, 0, 0);
+			int nd = 0;
+			if (cs.size() == 1) {
+				sum = sum + cs[0].cp;
+				nd = 1;
+			} else {
+				for (int k = 0; k + 1 < (int)cs.size(); k++) {
+					Q ttn = arc(cs[k].cp, cs[k + 1].cp);
+					V3 axis = get_axis(ttn);
+					double angle = get_angle(ttn) / 2.0;
+					V3 half = xform(axis_angle_basis(axis, (float)angle), cs[k].cp);
+					half = half * get_angle(ttn);
+					half = normalized(half);
+					sum = sum + half;
+					nd++;
+				}
+			}
+			V3 new_y = sum;
+			if (nd) new_y = normalized(divs(new_y, (float)nd));
+			int par = p.bone_ik_parent[b];
+			if (par >= 0) {
+				B3 gb = G[par].b * T[slot]; // twist node global = parent pose global * local
+				Q otn = arc(normalized(col(gb, 1)), normalized(xform(gb, new_y)));
+				B3 Pb = G[par].b;
+				T[slot] = ((inverse(Pb) * from_quat(otn)) * Pb) * T[slot];
+			}
+			for (auto &cone : cs) set_control_point(cone, normalized(cone.cp));
+			update_tangent_radii(cs);
+			kc[slot] = cs;
+		}
+		for (int slot = 0; slot < NC; slot++) {
+			auto put = [&](int f, float v) { p.CF[((size_t)slot * cfs + f) * N + s] = v; };
+			auto putd = [&](int f, double v) { p.CD[((size_t)slot * cds + f) * N + s] = v; };
+			put(CF_TWIST_Q + 0, tcr[slot].x);
+			put(CF_TWIST_Q + 1, tcr[slot].y);
+			put(CF_TWIST_Q + 2, tcr[slot].z);
+			put(CF_TWIST_Q + 3, tcr[slot].w);
+			put(CF_TWIST_COS, thc[slot]);
+			for (int f = 0; f < 9; f++) put(CF_TWIST_T + f, T[slot].r[f / 3][f % 3]);
+			for (int k = 0; k < (int)kc[slot].size(); k++) {
+				const Cone &c = kc[slot][k];
+				int o = CF_CONE0 + CF_PER_CONE * k;
+				put(o + 0, c.cp.x); put(o + 1, c.cp.y); put(o + 2, c.cp.z);
+				put(o + 3, (float)c.radius);
+				put(o + 4, c.t1.x); put(o + 5, c.t1.y); put(o + 6, c.t1.z);
+				put(o + 7, c.t2.x); put(o + 8, c.t2.y); put(o + 9, c.t2.z);
+				put(o + 10, (float)c.tr);
+				putd(CD_PER_CONE * k + 0, c.rcos);
+				putd(CD_PER_CONE * k + 1, c.trcos);
+			}
+		}
+	}
+	return "";
+}
+
+// ---------------------------------------------------------------------------------------
+// Launch shape + sibling-level schedule
+// ---------------------------------------------------------------------------------------
+int32_t lds_floats_per_skeleton(const HostPlan &p) { return p.B * 24 + p.P * 25; }
+
+static int ceil_log2(int v) {
+	int l = 0;
+	while ((1 << l) < v) l++;
+	return l;
+}
+
+void build_schedule(HostPlan &p, int32_t lanes, int64_t nlaunch) {
+	int maxh = 0;
+	for (int i = 0; i < p.NS; i++) maxh = std::max(maxh, p.seg_height[i]);
+	std::vector<std::vector<int>> lev(maxh + 1);
+	for (int i = 0; i < p.NS; i++) lev[p.seg_height[i]].push_back(i);
+	int widest = 1;
+	for (auto &l : lev) widest = std::max(widest, (int)l.size());
+	int K;
+	if (lanes > 0) {
+		K = 1 << ceil_log2(lanes);
+	} else {
+		K = std::min(64, 1 << ceil_log2(widest));
+		// Fill the chip: >= 4 waves' worth of blocks per CU-quad (1024 single-wave blocks).
+		while (K < 64 && (nlaunch + (64 / K) - 1) / (64 / K) < 1024) K *= 2;
+		// Keep at least ~3 blocks resident per CU (LDS 160 KiB).
+		while (K < 64 && (int64_t)(64 / K) * lds_floats_per_skeleton(p) * 4 > 48 * 1024) K *= 2;
+	}
+	K = std::max(1, std::min(64, K));
+	p.K = K;
+	p.log2K = ceil_log2(K);
+	p.spw = 64 / K;
+	while (p.spw > 1 && (int64_t)p.spw * ((lds_floats_per_skeleton(p) + 3) & ~3) * 4 > 160 * 1024) p.spw /= 2;
+	p.sched.clear();
+	p.nrows = 0;
+	for (auto &l : lev) {
+		for (size_t start = 0; start < l.size(); start += K) {
+			int cnt = (int)std::min<size_t>(K, l.size() - start);
+			int m = K >> ceil_log2(cnt);
+			std::vector<SchedTask> row(K, SchedTask{-1, 0, 1, 0});
+			for (int i = 0; i < cnt; i++)
+				for (int j = 0; j < m; j++) row[i * m + j] = SchedTask{l[start + i], j, m, 0};
+			p.sched.insert(p.sched.end(), row.begin(), row.end());
+			p.nrows++;
+		}
+	}
+}
+
+} // namespace mbik

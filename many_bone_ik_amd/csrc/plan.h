@@ -1,0 +1,95 @@
+// Flat, SoA plan for the batched solve: the output of ManyBoneIK3D::_bone_list_changed
+// (src/many_bone_ik_3d.cpp:1011-1068) for a topology shared by a batch of skeletons,
+// plus each skeleton's setup-dependent tables (bone directions, Kusudama frames).
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/mbik.h"
+
+namespace mbik {
+
+enum BoneFlags : int32_t {
+	BF_IN_LIST = 1,    // in ManyBoneIK3D::bone_list (solved and written back)
+	BF_ORIENT = 2,     // IK parent valid && orientationally constrained (ik_bone_segment_3d.cpp:156-159)
+	BF_AXIAL = 4,      // IK parent valid && axially constrained (:160-162)
+	BF_PINNED = 8,     // carries an IKEffector3D
+};
+
+enum SegFlags : int32_t {
+	SF_TRANSLATE = 1,  // root segment: translate=true, damp=PI (ik_bone_segment_3d.cpp:217-222)
+};
+
+// Pose-node parent codes (IKNode3D parent of godot_skeleton_aligned_transform).
+constexpr int32_t POSE_PARENT_NONE = -1;      // released ik_origin (earlier roots of a multi-root skeleton)
+constexpr int32_t POSE_PARENT_ORIGIN = -2;    // the live ik_origin (identity)
+
+// Per-skeleton float fields of one constraint slot: twist centre rotation (4), twist half-range
+// half-cosine (1), twist frame local basis (9), then per cone: control point (3), radius as real_t
+// (1), tangent centre 1 (3), tangent centre 2 (3), tangent radius as real_t (1).
+constexpr int CF_TWIST_Q = 0;
+constexpr int CF_TWIST_COS = 4;
+constexpr int CF_TWIST_T = 5;
+constexpr int CF_CONE0 = 14;
+constexpr int CF_PER_CONE = 11;
+// Per-skeleton double fields of one constraint slot, per cone: radius cosine, tangent radius cosine.
+constexpr int CD_PER_CONE = 2;
+
+struct SchedTask {
+	int32_t seg;  // -1 idle
+	int32_t j;    // index of this lane inside the segment's lane group
+	int32_t m;    // lanes in the group (power of two, aligned)
+	int32_t pad;
+};
+
+struct HostPlan {
+	// ---- topology (shared by the batch) ----
+	int32_t B = 0, P = 0, NS = 0, NC = 0, max_cones = 1;
+	int32_t iterations = 15;
+	int32_t constraint_mode = 0, stabilization_passes = 0;
+	std::vector<int32_t> parents;
+	std::vector<int32_t> bone_pose_parent, bone_ik_parent, bone_depth, bone_flags, bone_pin, bone_cons;
+	std::vector<int32_t> bone_list;                 // ManyBoneIK3D::bone_list order
+	std::vector<int32_t> bone_child_eff_off, bone_child_effs; // pinned IK children of each bone
+	// segments, numbered in creation order (parents before children)
+	std::vector<int32_t> seg_root, seg_tip, seg_parent;
+	std::vector<std::vector<int32_t>> seg_children;
+	std::vector<int32_t> seg_bone_off, seg_bones;   // tip -> root
+	std::vector<int32_t> seg_eff_off, seg_effs, seg_eff_hoff;
+	std::vector<int32_t> seg_nh, seg_flags, seg_hw_off, seg_height, seg_tin, seg_tout;
+	std::vector<double> seg_hw;                     // heading weights (recursive_create_penalty_array)
+	std::vector<double> seg_cos_half_damp;          // per (segment, bone position): cos(damp / 2.0)
+	std::vector<int32_t> roots;                     // root segments (segmented_skeletons)
+	std::vector<int32_t> eff_bone, eff_parent_bone, eff_path_off, eff_path;
+	std::vector<float> eff_prio;
+	std::vector<int32_t> cons_bone, cons_ncones;    // constraint slots (bones in the list only)
+	std::vector<int32_t> cons_order, cons_order_slot, cons_order_ncones; // applied constraints, desc order
+	int32_t desc_constraint_count = 0;
+	int32_t max_headings = 0;
+	// ---- launch shape ----
+	int32_t K = 4, log2K = 2, spw = 16;
+	std::vector<SchedTask> sched;                   // [nrows][K]
+	int32_t nrows = 0;
+	// ---- per skeleton, SoA [item][field][N] ----
+	int32_t N = 0;
+	std::vector<float> D;    // [B][9][N] bone-direction local basis
+	std::vector<float> CF;   // [NC][CF_CONE0 + CF_PER_CONE*max_cones][N]
+	std::vector<double> CD;  // [NC][CD_PER_CONE*max_cones][N]
+
+	int cf_stride() const { return CF_CONE0 + CF_PER_CONE * max_cones; }
+	int cd_stride() const { return CD_PER_CONE * max_cones; }
+};
+
+// Builds the topology tables; returns an empty string on success, else the error.
+std::string build_topology(const mbik_skeleton_desc &desc, const mbik_config &cfg, HostPlan &plan);
+// Fills D / CF / CD for skeletons [0, n) from their setup poses, cones and twist.
+std::string build_skeletons(HostPlan &plan, int32_t n, const float *setup_pose, const float *cones, const float *twist,
+		int32_t max_cones_in);
+// Chooses lanes-per-skeleton / skeletons-per-block and the sibling-level schedule.
+void build_schedule(HostPlan &plan, int32_t lanes_per_skeleton, int64_t skeletons_in_launch);
+// LDS floats per skeleton used by the kernel.
+int32_t lds_floats_per_skeleton(const HostPlan &plan);
+
+} // namespace mbik

@@ -1,0 +1,139 @@
+"""Host-side plan/solve wrapper over the C ABI (include/mbik.h).
+
+`Plan` owns one `mbik_plan` (topology tables + per-skeleton setup data resident on one
+GPU).  `solve()` takes device pointers (e.g. torch CUDA tensors' data_ptr()) and is
+asynchronous on the given HIP stream; `solve_host()` takes numpy arrays.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+
+import numpy as np
+
+from . import _lib
+from ._lib import MbikConfig, MbikConstraint, MbikPin, MbikPlanInfo, MbikSkeletonDesc, check
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+class Plan:
+    """== ManyBoneIK3D after _bone_list_changed(), for a batch of same-topology skeletons."""
+
+    def __init__(self, parents, pins, constraints, setup_pose, cones=None, twist=None, *,
+                 iterations=15, default_damp=math.radians(5.0), constraint_mode=False,
+                 stabilization_passes=0, bone_damp=None, max_cones=None, device=0, lanes=0):
+        L = _lib.load()
+        self._L = L
+        parents = np.ascontiguousarray(parents, np.int32)
+        B = parents.shape[0]
+        setup_pose = np.ascontiguousarray(setup_pose, np.float32)
+        n = setup_pose.shape[0]
+        assert setup_pose.shape == (n, B, 10), setup_pose.shape
+        pin_arr = (MbikPin * max(1, len(pins)))()
+        for i, p in enumerate(pins):
+            pin_arr[i].bone = int(p["bone"])
+            pin_arr[i].weight = float(p.get("weight", 0.0))
+            pr = p.get("direction_priorities", (0.2, 0.0, 0.2))
+            for a in range(3):
+                pin_arr[i].direction_priorities[a] = float(pr[a])
+            pin_arr[i].motion_propagation_factor = float(p.get("motion_propagation_factor", 1.0))
+        con_arr = (MbikConstraint * max(1, len(constraints)))()
+        for i, c in enumerate(constraints):
+            con_arr[i].bone = int(c["bone"])
+            con_arr[i].cone_count = int(c.get("cone_count", 0))
+        mc = max_cones if max_cones is not None else (cones.shape[2] if cones is not None and cones.ndim == 4 else 1)
+        desc = MbikSkeletonDesc()
+        desc.bone_count = B
+        desc.parents = parents.ctypes.data_as(C.POINTER(C.c_int32))
+        desc.pin_count = len(pins)
+        desc.pins = C.cast(pin_arr, C.POINTER(MbikPin))
+        desc.constraint_count = len(constraints)
+        desc.constraints = C.cast(con_arr, C.POINTER(MbikConstraint))
+        desc.max_cones = int(mc)
+        cfg = MbikConfig()
+        cfg.iterations_per_frame = int(iterations)
+        cfg.default_damp = float(default_damp)
+        cfg.constraint_mode = int(bool(constraint_mode))
+        cfg.stabilization_passes = int(stabilization_passes)
+        bd = None if bone_damp is None else np.ascontiguousarray(bone_damp, np.float32)
+        cfg.bone_damp_count = 0 if bd is None else bd.shape[0]
+        cfg.bone_damp = None if bd is None else bd.ctypes.data_as(C.POINTER(C.c_float))
+        cones_a = None if cones is None else np.ascontiguousarray(cones, np.float32)
+        twist_a = None if twist is None else np.ascontiguousarray(twist, np.float32)
+        h = C.c_void_p()
+        check(L.mbik_plan_create(C.byref(desc), C.byref(cfg), n, _ptr(setup_pose), _ptr(cones_a), _ptr(twist_a),
+                                 int(device), C.byref(h)))
+        self.h = h
+        self.n = n
+        self.B = B
+        self.P = len(pins)
+        self.iterations = int(iterations)
+        if lanes:
+            self.set_launch(lanes)
+
+    @classmethod
+    def from_workload(cls, wl, device=0, lanes=0, iterations=None):
+        t = wl.topo
+        pins = [dict(bone=int(b), weight=wl.pin_weight, direction_priorities=wl.pin_priority,
+                     motion_propagation_factor=wl.pin_propagation) for b in t.pins]
+        cons = [dict(bone=int(b), cone_count=t.cones_per_bone) for b in t.constrained]
+        return cls(t.parents, pins, cons, wl.pose, wl.cones, wl.twist,
+                   iterations=t.iterations if iterations is None else iterations,
+                   default_damp=wl.default_damp, max_cones=wl.cones.shape[2], device=device, lanes=lanes)
+
+    def info(self) -> dict:
+        inf = MbikPlanInfo()
+        check(self._L.mbik_plan_get_info(self.h, C.byref(inf)))
+        return {f: getattr(inf, f) for f, _ in MbikPlanInfo._fields_}
+
+    def set_launch(self, lanes: int):
+        check(self._L.mbik_plan_set_launch(self.h, int(lanes)))
+
+    def solve(self, pose_in_ptr: int, targets_ptr: int, pose_out_ptr: int, first: int = 0, count: int | None = None,
+              stream: int = 0):
+        count = self.n - first if count is None else count
+        check(self._L.mbik_solve(self.h, first, count, C.c_void_p(pose_in_ptr), C.c_void_p(targets_ptr),
+                                 C.c_void_p(pose_out_ptr), C.c_void_p(stream or None)))
+
+    def segment_solve(self, segment: int, pose_ptr: int, targets_ptr: int, first: int = 0, count: int | None = None,
+                      stream: int = 0):
+        count = self.n - first if count is None else count
+        check(self._L.mbik_segment_solve(self.h, segment, first, count, C.c_void_p(pose_ptr), C.c_void_p(targets_ptr),
+                                         C.c_void_p(stream or None)))
+
+    def solve_host(self, pose_in, targets, first: int = 0) -> np.ndarray:
+        pose_in = np.ascontiguousarray(pose_in, np.float32)
+        targets = np.ascontiguousarray(targets, np.float32)
+        count = pose_in.shape[0]
+        assert pose_in.shape == (count, self.B, 10)
+        assert targets.shape == (count, self.P, 12)
+        out = np.empty_like(pose_in)
+        check(self._L.mbik_solve_host(self.h, first, count, _ptr(pose_in), _ptr(targets), _ptr(out)))
+        return out
+
+    def segment_table(self):
+        n = self.info()["segment_count"]
+        r = np.zeros(n, np.int32); t = np.zeros(n, np.int32); p = np.zeros(n, np.int32)
+        check(self._L.mbik_plan_segment_table(self.h, _ptr(r), _ptr(t), _ptr(p), n))
+        return r, t, p
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._L.mbik_plan_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def quat_error(a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    """Per-bone sign-invariant quaternion error min(|q-r|_inf, |q+r|_inf)."""
+    qa = a[..., 0:4].astype(np.float64)
+    qb = b[..., 0:4].astype(np.float64)
+    return np.minimum(np.abs(qa - qb).max(-1), np.abs(qa + qb).max(-1))

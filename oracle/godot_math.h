@@ -30,6 +30,23 @@
 #define GD_PI 3.1415926535897932384626433833
 #define GD_TAU 6.2831853071795864769252867666
 
+/* Float transcendentals.  Godot's Math::sin/cos/acos(float) call the platform libm
+ * (sinf/cosf/acosf), whose last-ulp behaviour differs between libms (glibc, MSVC, ...).
+ * The reference's dynamics amplify a 1-ulp difference ~2x per iteration, so the oracle
+ * pins the rounding: by default each is evaluated in double and rounded once (correctly
+ * rounded except in rare double-rounding cases), which the GPU path reproduces.  Build
+ * with -DORACLE_PLATFORM_LIBM to call the platform libm instead (DESIGN.md quantifies the
+ * spread between the two). */
+#ifdef ORACLE_PLATFORM_LIBM
+static inline float gd_sinf(float x) { return sinf(x); }
+static inline float gd_cosf(float x) { return cosf(x); }
+static inline float gd_acosf(float x) { return acosf(x); }
+#else
+static inline float gd_sinf(float x) { return (float)sin((double)x); }
+static inline float gd_cosf(float x) { return (float)cos((double)x); }
+static inline float gd_acosf(float x) { return (float)acos((double)x); }
+#endif
+
 typedef struct { float x, y, z; } v3;
 typedef struct { float x, y, z, w; } quat;
 typedef struct { v3 rows[3]; } basis;
@@ -109,8 +126,8 @@ static inline int q_is_finite(quat q) { return isfinite(q.x) && isfinite(q.y) &&
 static inline quat q_axis_angle(v3 axis, float angle) {
 	float d = v3_length(axis);
 	if (d == 0) return q_make(0, 0, 0, 0);
-	float sin_angle = sinf(angle * 0.5f);
-	float cos_angle = cosf(angle * 0.5f);
+	float sin_angle = gd_sinf(angle * 0.5f);
+	float cos_angle = gd_cosf(angle * 0.5f);
 	float s = sin_angle / d;
 	return q_make(axis.x * s, axis.y * s, axis.z * s, cos_angle);
 }
@@ -135,7 +152,7 @@ static inline v3 q_get_axis(quat q) {
 	float r = ((float)1) / sqrtf(1 - q.w * q.w);
 	return v3_make(q.x * r, q.y * r, q.z * r);
 }
-static inline float q_get_angle(quat q) { return 2 * acosf(q.w); }
+static inline float q_get_angle(quat q) { return 2 * gd_acosf(q.w); }
 /* Quaternion::slerp (Godot 4.3); note the (1.0 - weight) * omega term is double. */
 static inline quat q_slerp(quat from, quat to, float weight) {
 	quat to1;
@@ -148,10 +165,10 @@ static inline quat q_slerp(quat from, quat to, float weight) {
 		to1 = to;
 	}
 	if ((1.0f - cosom) > (float)GD_CMP_EPSILON) {
-		omega = acosf(cosom);
-		sinom = sinf(omega);
+		omega = gd_acosf(cosom);
+		sinom = gd_sinf(omega);
 		scale0 = (float)(sin((1.0 - weight) * omega) / sinom);
-		scale1 = sinf(weight * omega) / sinom;
+		scale1 = gd_sinf(weight * omega) / sinom;
 	} else {
 		scale0 = 1.0f - weight;
 		scale1 = weight;
@@ -290,11 +307,11 @@ static inline v3 b_get_scale(basis b) {
 static inline basis b_axis_angle(v3 axis, float angle) {
 	basis b;
 	v3 sq = v3_make(axis.x * axis.x, axis.y * axis.y, axis.z * axis.z);
-	float cosine = cosf(angle);
+	float cosine = gd_cosf(angle);
 	b.rows[0].x = sq.x + cosine * (1.0f - sq.x);
 	b.rows[1].y = sq.y + cosine * (1.0f - sq.y);
 	b.rows[2].z = sq.z + cosine * (1.0f - sq.z);
-	float sine = sinf(angle);
+	float sine = gd_sinf(angle);
 	float t = 1 - cosine;
 	float xyzt = axis.x * axis.y * t;
 	float zyxs = axis.z * sine;

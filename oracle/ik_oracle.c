@@ -291,8 +291,8 @@ static void cone_set_radius(cone_t *c, double r) {
 static quat quat_axis_angle_sq(v3 axis, float angle) {
 	float d = v3_length_squared(axis);
 	if (d == 0) return q_identity();
-	float sin_angle = sinf(angle * 0.5f);
-	float cos_angle = cosf(angle * 0.5f);
+	float sin_angle = gd_sinf(angle * 0.5f);
+	float cos_angle = gd_cosf(angle * 0.5f);
 	float s = sin_angle / d;
 	return q_make(axis.x * s, axis.y * s, axis.z * s, cos_angle);
 }
@@ -457,7 +457,7 @@ static void kusudama_set_axial_limits(kusudama_t *k, float min_angle, float in_r
 	k->twist_min_vec = v3_normalized(q_xform(k->twist_min_rot, z_axis));
 	k->twist_center_vec = v3_normalized(q_xform(k->twist_min_rot, k->twist_min_vec));
 	k->twist_center_rot = q_arc(z_axis, k->twist_center_vec);
-	k->twist_half_range_half_cos = cosf(in_range / (float)4.0);
+	k->twist_half_range_half_cos = gd_cosf(in_range / (float)4.0);
 	k->twist_max_vec = v3_normalized(q_xform(quat_axis_angle_sq(y_axis, in_range), k->twist_min_vec));
 	k->twist_max_rot = q_arc(z_axis, k->twist_max_vec);
 }
@@ -797,7 +797,7 @@ static void bone_create(skel_t *s, int id, int parent, float default_dampening) 
 	b->pose = node_new(s);
 	b->bdir = node_new(s);
 	b->default_dampening = default_dampening;
-	b->cos_half_dampen = cosf(default_dampening / (float)2.0);
+	b->cos_half_dampen = gd_cosf(default_dampening / (float)2.0);
 	if (parent >= 0) bone_set_parent(s, id, parent);
 	const oracle_desc *d = s->desc;
 	for (int i = 0; i < d->pin_count; i++) {
