@@ -1,0 +1,211 @@
+#!/usr/bin/env python3
+"""Benchmark: skeletons/s solved to convergence (fixed 16 iterations) on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2]
+
+One *step* = one mbik_solve() over this rank's batch of skeletons (BASELINE.json
+configs[1] = C2 by default: 4096 x 32 bones / 4 effectors / 2 Kusudama cones per bone,
+16 iterations), inputs already resident in HBM.  N > 1 is launched by
+torch.distributed.run, one rank per GPU; every rank solves its own shard of skeletons
+(weak scaling, no collective on the data path) and an RCCL all_gather of the output poses
+is timed separately after the solve loop ("gather_ms").  Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
+SKEL_PER_GPU = {2: 4096, 3: 65536, 4: 262144 // 8, 5: 16384}
+METRIC = "skeletons/sec to convergence (32-bone/4-eff, 16 iters) at 1/2/4/8 GPU; bone-quat max-err vs ref"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5])
+    ap.add_argument("--skeletons", type=int, default=0, help="skeletons per GPU (default: the config's)")
+    ap.add_argument("--lanes", type=int, default=0, help="lanes per skeleton override (0 = plan default)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample budget")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(HERE, "profiles", "traffic.json"))
+    return ap.parse_args()
+
+
+def cpu_baseline(cfg: int, seconds: float):
+    """Oracle (plain-C restatement of the reference) on the host cores, bounded sample."""
+    from many_bone_ik_amd import workloads as W
+    from oracle import pyoracle as po
+    threads = max(1, min(16, os.cpu_count() or 1))
+    n = 512 if cfg in (2, 3, 4) else 64
+    wl = W.generate(cfg, n)
+    o = po.Oracle(wl)
+    done = 0
+    t0 = time.perf_counter()
+    while True:
+        o.solve(wl.pose, wl.targets, threads=threads)
+        done += n
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    o.close()
+    return {"value": done / el, "unit": "skeletons/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/ (C restatement of the reference solve, reference object model) on config C{cfg}: "
+                      f"{n} skeletons solved {done // n} times in {el:.1f} s with {threads} threads"}
+
+
+def main():
+    args = parse()
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world > 1:
+        print(f"warning: WORLD_SIZE={world} != --gpus {args.gpus}", file=sys.stderr)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist_mod
+        dist = dist_mod
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    else:
+        torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+
+    from many_bone_ik_amd import workloads as W
+    from many_bone_ik_amd.solver import Plan, quat_error
+
+    cfg = args.config
+    n = args.skeletons or SKEL_PER_GPU[cfg]
+    first = rank * n
+    wl = W.generate(cfg, n, first=first)
+    plan = Plan.from_workload(wl, device=local_rank, lanes=args.lanes)
+    info = plan.info()
+    pose_in = torch.from_numpy(wl.pose).to(dev)
+    targets = torch.from_numpy(wl.targets).to(dev)
+    pose_out = torch.empty_like(pose_in)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        plan.solve(pose_in.data_ptr(), targets.data_ptr(), pose_out.data_ptr(), 0, n, stream.cuda_stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    kernel_ms = ev0.elapsed_time(ev1) / max(1, args.steps)
+    elapsed = torch.tensor([wall], dtype=torch.float64, device=dev)
+    if dist:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    wall_max = float(elapsed.item())
+
+    gather_ms = None
+    if dist:
+        parts = [torch.empty_like(pose_out) for _ in range(world)]
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        g0 = time.perf_counter()
+        dist.all_gather(parts, pose_out)
+        torch.cuda.synchronize(dev)
+        gt = torch.tensor([time.perf_counter() - g0], dtype=torch.float64, device=dev)
+        dist.all_reduce(gt, op=dist.ReduceOp.MAX)
+        gather_ms = float(gt.item()) * 1e3
+
+    # parity spot check of this rank's first skeletons against the oracle (not timed)
+    parity = None
+    if not args.no_parity and rank == 0:
+        try:
+            from oracle import pyoracle as po
+            k = min(64, n)
+            sub = W.generate(cfg, k, first=first)
+            o = po.Oracle(sub)
+            ref = o.solve(sub.pose, sub.targets, threads=max(1, min(16, os.cpu_count() or 1)))
+            got = pose_out[:k].cpu().numpy()
+            qe = quat_error(got, ref)
+            parity = {"skeletons": k, "max_quat_err": float(qe.max()),
+                      "frac_skeletons_le_1e-4": float(np.mean(qe.max(-1) <= 1e-4)),
+                      "bitwise_equal": bool(np.array_equal(got.view(np.uint32), ref.view(np.uint32)))}
+        except Exception as e:  # oracle missing on the box: report, never fall back
+            parity = {"error": str(e)}
+
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+    total = n * world
+    ms_per_step = wall_max / args.steps * 1e3
+    value = total / (wall_max / args.steps)
+    alg_bytes = info["algorithmic_bytes_per_skeleton"] * n
+    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            tj = json.load(open(args.traffic_json))
+            key = f"c{cfg}_{n}"
+            if key in tj:
+                traffic = tj[key]["hbm_bytes_per_launch"]
+        except Exception:
+            traffic = None
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "skeletons/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (seeded generator, many_bone_ik_amd/workloads.py)",
+        "config": {"workload": W.bench_config_name(cfg), "baseline_config": f"configs[{cfg - 1}]",
+                   "skeletons_per_gpu": n, "bones": wl.bone_count, "effectors": int(wl.topo.pins.shape[0]),
+                   "cones_per_bone": wl.topo.cones_per_bone, "iterations": wl.topo.iterations,
+                   "lanes_per_skeleton": info["lanes_per_skeleton"], "skeletons_per_block": info["skeletons_per_block"],
+                   "parallelism": f"dp{world} (skeleton shards, no data-path collective)"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "algorithmic_bytes_per_launch": alg_bytes, "kernel_ms": kernel_ms,
+                     "note": "latency/VALU-bound serial chain; HBM fraction reported as requested (DESIGN.md §5)"},
+        "gather_ms": gather_ms,
+        "parity": parity,
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
+        except Exception as e:
+            out["cpu_baseline"] = {"error": str(e)}
+    print(json.dumps(out))
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -131,6 +131,14 @@ int32_t mbik_segment_solve(mbik_plan *plan, int32_t segment, int32_t first, int3
 int32_t mbik_plan_segment_table(const mbik_plan *plan, int32_t *root_bone, int32_t *tip_bone, int32_t *parent_segment,
 		int32_t capacity);
 
+/* Host-only (no device needed): runs the _bone_list_changed segmentation for `desc` and
+ * reports the solve order.  bone_list receives ManyBoneIK3D::bone_list (capacity
+ * bone_count), segment_* receive the post-order segment table (capacity bone_count), and
+ * segment_headings the heading count of each segment.  Returns the segment count. */
+int32_t mbik_describe_topology(const mbik_skeleton_desc *desc, const mbik_config *config, int32_t *bone_list,
+		int32_t *bone_list_count, int32_t *segment_root, int32_t *segment_tip, int32_t *segment_parent,
+		int32_t *segment_headings);
+
 const char *mbik_last_error(void);
 
 #ifdef __cplusplus

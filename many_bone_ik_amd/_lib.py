@@ -20,7 +20,8 @@ MBIK_ENODEV = -5
 
 EXPORTED_SYMBOLS = (
     "mbik_plan_create", "mbik_plan_destroy", "mbik_plan_get_info", "mbik_plan_set_launch",
-    "mbik_solve", "mbik_solve_host", "mbik_segment_solve", "mbik_plan_segment_table", "mbik_last_error",
+    "mbik_solve", "mbik_solve_host", "mbik_segment_solve", "mbik_plan_segment_table", "mbik_describe_topology",
+    "mbik_last_error",
 )
 
 
@@ -68,6 +69,13 @@ def load():
     global _lib
     if _lib is not None:
         return _lib
+    try:
+        # torch's ROCm wheel bundles its own libamdhip64.so.7 (same SONAME as /opt/rocm's).
+        # Whichever is loaded first is shared by the process; torch only works on its own,
+        # and libmbik's gfx950 code object runs on either, so let torch's load first.
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"{LIB_PATH} is missing: build it with `python -m many_bone_ik_amd.build` "
                           "(the HIP path has no CPU fallback)")
@@ -90,6 +98,8 @@ def load():
     L.mbik_segment_solve.restype = C.c_int32
     L.mbik_plan_segment_table.argtypes = [vp, vp, vp, vp, C.c_int32]
     L.mbik_plan_segment_table.restype = C.c_int32
+    L.mbik_describe_topology.argtypes = [C.POINTER(MbikSkeletonDesc), C.POINTER(MbikConfig), vp, vp, vp, vp, vp, vp]
+    L.mbik_describe_topology.restype = C.c_int32
     L.mbik_last_error.argtypes = []
     L.mbik_last_error.restype = C.c_char_p
     _lib = L

@@ -117,6 +117,20 @@ GDI Q axis_angle_sq(V3 axis, float angle) {
 	float s = sin_angle / d;
 	return q4(axis.x * s, axis.y * s, axis.z * s, cos_angle);
 }
+// The two constructors above with sin/cos of the half angle precomputed (for per-cone
+// constant angles: the plan stores them, the solve never re-evaluates the trig).
+GDI Q axis_angle_sc(V3 axis, float sin_half, float cos_half) {
+	float d = length(axis);
+	if (d == 0) return q4(0, 0, 0, 0);
+	float s = sin_half / d;
+	return q4(axis.x * s, axis.y * s, axis.z * s, cos_half);
+}
+GDI Q axis_angle_sq_sc(V3 axis, float sin_half, float cos_half) {
+	float d = length_sq(axis);
+	if (d == 0) return qid();
+	float s = sin_half / d;
+	return q4(axis.x * s, axis.y * s, axis.z * s, cos_half);
+}
 // Quaternion(v0, v1) shortest arc (Godot 4.3: normalising form)
 GDI Q arc(V3 v0, V3 v1) {
 	const float ALMOST_ONE = 1.0f - (float)CMP_EPSILON;
@@ -161,7 +175,8 @@ GDI B3 from_quat(Q q) {
 	float yy = q.y * ys, yz = q.y * zs, zz = q.z * zs;
 	return bset(1.0f - (yy + zz), xy - wz, xz + wy, xy + wz, 1.0f - (xx + zz), yz - wx, xz - wy, yz + wx, 1.0f - (xx + yy));
 }
-// Basis::get_quaternion
+// Basis::get_quaternion (the major-diagonal branch is spelled out per case so that no
+// runtime-indexed array exists -- on the GPU that would live in scratch memory).
 GDI Q get_quaternion(const B3 &m) {
 	float r00 = m.r[0].x, r11 = m.r[1].y, r22 = m.r[2].z;
 	float trace = r00 + r11 + r22;
@@ -171,16 +186,23 @@ GDI Q get_quaternion(const B3 &m) {
 		s = 0.5f / s;
 		return q4((m.r[2].y - m.r[1].z) * s, (m.r[0].z - m.r[2].x) * s, (m.r[1].x - m.r[0].y) * s, w);
 	}
-	float t[4];
 	int i = r00 < r11 ? (r11 < r22 ? 2 : 1) : (r00 < r22 ? 2 : 0);
-	int j = (i + 1) % 3, k = (i + 2) % 3;
-	float s = sqrtf(at(m, i, i) - at(m, j, j) - at(m, k, k) + 1.0f);
-	t[i] = s * 0.5f;
-	s = 0.5f / s;
-	t[3] = (at(m, k, j) - at(m, j, k)) * s;
-	t[j] = (at(m, j, i) + at(m, i, j)) * s;
-	t[k] = (at(m, k, i) + at(m, i, k)) * s;
-	return q4(t[0], t[1], t[2], t[3]);
+	if (i == 0) { // j = 1, k = 2
+		float s = sqrtf(r00 - r11 - r22 + 1.0f);
+		float ti = s * 0.5f;
+		s = 0.5f / s;
+		return q4(ti, (m.r[1].x + m.r[0].y) * s, (m.r[2].x + m.r[0].z) * s, (m.r[2].y - m.r[1].z) * s);
+	} else if (i == 1) { // j = 2, k = 0
+		float s = sqrtf(r11 - r22 - r00 + 1.0f);
+		float ti = s * 0.5f;
+		s = 0.5f / s;
+		return q4((m.r[0].y + m.r[1].x) * s, ti, (m.r[2].y + m.r[1].z) * s, (m.r[0].z - m.r[2].x) * s);
+	} else { // i = 2: j = 0, k = 1
+		float s = sqrtf(r22 - r00 - r11 + 1.0f);
+		float ti = s * 0.5f;
+		s = 0.5f / s;
+		return q4((m.r[0].z + m.r[2].x) * s, (m.r[1].z + m.r[2].y) * s, ti, (m.r[1].x - m.r[0].y) * s);
+	}
 }
 // Basis::orthonormalize (Gram-Schmidt on columns)
 GDI B3 orthonormalized(const B3 &b) {

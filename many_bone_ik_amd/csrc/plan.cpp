@@ -540,11 +540,12 @@ std::string build_skeletons(HostPlan &p, int32_t n, const float *setup_pose, con
 			for (int k = 0; k < (int)kc[slot].size(); k++) {
 				const Cone &c = kc[slot][k];
 				int o = CF_CONE0 + CF_PER_CONE * k;
-				put(o + 0, c.cp.x); put(o + 1, c.cp.y); put(o + 2, c.cp.z);
-				put(o + 3, (float)c.radius);
-				put(o + 4, c.t1.x); put(o + 5, c.t1.y); put(o + 6, c.t1.z);
-				put(o + 7, c.t2.x); put(o + 8, c.t2.y); put(o + 9, c.t2.z);
-				put(o + 10, (float)c.tr);
+				float rf = (float)c.radius, trf = (float)c.tr;
+				put(o + CFC_CP + 0, c.cp.x); put(o + CFC_CP + 1, c.cp.y); put(o + CFC_CP + 2, c.cp.z);
+				put(o + CFC_SR, sin_f(rf * 0.5f)); put(o + CFC_CR, cos_f(rf * 0.5f));
+				put(o + CFC_T1 + 0, c.t1.x); put(o + CFC_T1 + 1, c.t1.y); put(o + CFC_T1 + 2, c.t1.z);
+				put(o + CFC_T2 + 0, c.t2.x); put(o + CFC_T2 + 1, c.t2.y); put(o + CFC_T2 + 2, c.t2.z);
+				put(o + CFC_ST, sin_f(trf * 0.5f)); put(o + CFC_CT, cos_f(trf * 0.5f));
 				putd(CD_PER_CONE * k + 0, c.rcos);
 				putd(CD_PER_CONE * k + 1, c.trcos);
 			}

@@ -27,13 +27,16 @@ constexpr int32_t POSE_PARENT_NONE = -1;      // released ik_origin (earlier roo
 constexpr int32_t POSE_PARENT_ORIGIN = -2;    // the live ik_origin (identity)
 
 // Per-skeleton float fields of one constraint slot: twist centre rotation (4), twist half-range
-// half-cosine (1), twist frame local basis (9), then per cone: control point (3), radius as real_t
-// (1), tangent centre 1 (3), tangent centre 2 (3), tangent radius as real_t (1).
+// half-cosine (1), twist frame local basis (9), then per cone: control point (3), sin/cos of
+// half the radius (2), tangent centre 1 (3), tangent centre 2 (3), sin/cos of half the tangent
+// radius (2).  The half-angle sin/cos are what Quaternion(axis, angle) and
+// get_quaternion_axis_angle evaluate on the cone's constant angles (ik_open_cone_3d.cpp:297,312,371).
 constexpr int CF_TWIST_Q = 0;
 constexpr int CF_TWIST_COS = 4;
 constexpr int CF_TWIST_T = 5;
 constexpr int CF_CONE0 = 14;
-constexpr int CF_PER_CONE = 11;
+constexpr int CF_PER_CONE = 13;
+constexpr int CFC_CP = 0, CFC_SR = 3, CFC_CR = 4, CFC_T1 = 5, CFC_T2 = 8, CFC_ST = 11, CFC_CT = 12;
 // Per-skeleton double fields of one constraint slot, per cone: radius cosine, tangent radius cosine.
 constexpr int CD_PER_CONE = 2;
 

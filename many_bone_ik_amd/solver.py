@@ -19,6 +19,58 @@ def _ptr(a):
     return None if a is None else a.ctypes.data_as(C.c_void_p)
 
 
+class _Desc:
+    """Keeps the ctypes structures (and the arrays they point into) alive together."""
+
+    def __init__(self, parents, pins, constraints, max_cones, iterations, default_damp, constraint_mode,
+                 stabilization_passes, bone_damp):
+        self.parents = np.ascontiguousarray(parents, np.int32)
+        B = self.parents.shape[0]
+        self.pin_arr = (MbikPin * max(1, len(pins)))()
+        for i, p in enumerate(pins):
+            self.pin_arr[i].bone = int(p["bone"])
+            self.pin_arr[i].weight = float(p.get("weight", 0.0))
+            pr = p.get("direction_priorities", (0.2, 0.0, 0.2))
+            for a in range(3):
+                self.pin_arr[i].direction_priorities[a] = float(pr[a])
+            self.pin_arr[i].motion_propagation_factor = float(p.get("motion_propagation_factor", 1.0))
+        self.con_arr = (MbikConstraint * max(1, len(constraints)))()
+        for i, c in enumerate(constraints):
+            self.con_arr[i].bone = int(c["bone"])
+            self.con_arr[i].cone_count = int(c.get("cone_count", 0))
+        d = MbikSkeletonDesc()
+        d.bone_count = B
+        d.parents = self.parents.ctypes.data_as(C.POINTER(C.c_int32))
+        d.pin_count = len(pins)
+        d.pins = C.cast(self.pin_arr, C.POINTER(MbikPin))
+        d.constraint_count = len(constraints)
+        d.constraints = C.cast(self.con_arr, C.POINTER(MbikConstraint))
+        d.max_cones = int(max_cones)
+        self.desc = d
+        cfg = MbikConfig()
+        cfg.iterations_per_frame = int(iterations)
+        cfg.default_damp = float(default_damp)
+        cfg.constraint_mode = int(bool(constraint_mode))
+        cfg.stabilization_passes = int(stabilization_passes)
+        self.bd = None if bone_damp is None else np.ascontiguousarray(bone_damp, np.float32)
+        cfg.bone_damp_count = 0 if self.bd is None else self.bd.shape[0]
+        cfg.bone_damp = None if self.bd is None else self.bd.ctypes.data_as(C.POINTER(C.c_float))
+        self.cfg = cfg
+
+
+def describe_topology(parents, pins, constraints=(), *, iterations=15, default_damp=math.radians(5.0),
+                      bone_damp=None) -> dict:
+    """Host-only segmentation (mbik_describe_topology): bone_list + post-order segment table."""
+    L = _lib.load()
+    d = _Desc(parents, pins, list(constraints), 1, iterations, default_damp, False, 0, bone_damp)
+    B = d.parents.shape[0]
+    bl = np.zeros(B, np.int32); nbl = C.c_int32(0)
+    r = np.zeros(B, np.int32); t = np.zeros(B, np.int32); p = np.zeros(B, np.int32); nh = np.zeros(B, np.int32)
+    ns = check(L.mbik_describe_topology(C.byref(d.desc), C.byref(d.cfg), _ptr(bl), C.byref(nbl), _ptr(r), _ptr(t),
+                                        _ptr(p), _ptr(nh)))
+    return dict(bone_list=bl[:nbl.value], seg_root=r[:ns], seg_tip=t[:ns], seg_parent=p[:ns], seg_headings=nh[:ns])
+
+
 class Plan:
     """== ManyBoneIK3D after _bone_list_changed(), for a batch of same-topology skeletons."""
 
@@ -27,44 +79,16 @@ class Plan:
                  stabilization_passes=0, bone_damp=None, max_cones=None, device=0, lanes=0):
         L = _lib.load()
         self._L = L
-        parents = np.ascontiguousarray(parents, np.int32)
-        B = parents.shape[0]
         setup_pose = np.ascontiguousarray(setup_pose, np.float32)
-        n = setup_pose.shape[0]
+        n, B = setup_pose.shape[0], np.asarray(parents).shape[0]
         assert setup_pose.shape == (n, B, 10), setup_pose.shape
-        pin_arr = (MbikPin * max(1, len(pins)))()
-        for i, p in enumerate(pins):
-            pin_arr[i].bone = int(p["bone"])
-            pin_arr[i].weight = float(p.get("weight", 0.0))
-            pr = p.get("direction_priorities", (0.2, 0.0, 0.2))
-            for a in range(3):
-                pin_arr[i].direction_priorities[a] = float(pr[a])
-            pin_arr[i].motion_propagation_factor = float(p.get("motion_propagation_factor", 1.0))
-        con_arr = (MbikConstraint * max(1, len(constraints)))()
-        for i, c in enumerate(constraints):
-            con_arr[i].bone = int(c["bone"])
-            con_arr[i].cone_count = int(c.get("cone_count", 0))
-        mc = max_cones if max_cones is not None else (cones.shape[2] if cones is not None and cones.ndim == 4 else 1)
-        desc = MbikSkeletonDesc()
-        desc.bone_count = B
-        desc.parents = parents.ctypes.data_as(C.POINTER(C.c_int32))
-        desc.pin_count = len(pins)
-        desc.pins = C.cast(pin_arr, C.POINTER(MbikPin))
-        desc.constraint_count = len(constraints)
-        desc.constraints = C.cast(con_arr, C.POINTER(MbikConstraint))
-        desc.max_cones = int(mc)
-        cfg = MbikConfig()
-        cfg.iterations_per_frame = int(iterations)
-        cfg.default_damp = float(default_damp)
-        cfg.constraint_mode = int(bool(constraint_mode))
-        cfg.stabilization_passes = int(stabilization_passes)
-        bd = None if bone_damp is None else np.ascontiguousarray(bone_damp, np.float32)
-        cfg.bone_damp_count = 0 if bd is None else bd.shape[0]
-        cfg.bone_damp = None if bd is None else bd.ctypes.data_as(C.POINTER(C.c_float))
+        mc = max_cones if max_cones is not None else (cones.shape[2] if cones is not None and np.ndim(cones) == 4 else 1)
+        d = _Desc(parents, pins, list(constraints), mc, iterations, default_damp, constraint_mode,
+                  stabilization_passes, bone_damp)
         cones_a = None if cones is None else np.ascontiguousarray(cones, np.float32)
         twist_a = None if twist is None else np.ascontiguousarray(twist, np.float32)
         h = C.c_void_p()
-        check(L.mbik_plan_create(C.byref(desc), C.byref(cfg), n, _ptr(setup_pose), _ptr(cones_a), _ptr(twist_a),
+        check(L.mbik_plan_create(C.byref(d.desc), C.byref(d.cfg), n, _ptr(setup_pose), _ptr(cones_a), _ptr(twist_a),
                                  int(device), C.byref(h)))
         self.h = h
         self.n = n
@@ -77,12 +101,10 @@ class Plan:
     @classmethod
     def from_workload(cls, wl, device=0, lanes=0, iterations=None):
         t = wl.topo
-        pins = [dict(bone=int(b), weight=wl.pin_weight, direction_priorities=wl.pin_priority,
-                     motion_propagation_factor=wl.pin_propagation) for b in t.pins]
-        cons = [dict(bone=int(b), cone_count=t.cones_per_bone) for b in t.constrained]
-        return cls(t.parents, pins, cons, wl.pose, wl.cones, wl.twist,
+        return cls(t.parents, wl.pins(), wl.constraints(), wl.pose, wl.cones, wl.twist,
                    iterations=t.iterations if iterations is None else iterations,
-                   default_damp=wl.default_damp, max_cones=wl.cones.shape[2], device=device, lanes=lanes)
+                   default_damp=wl.default_damp, max_cones=wl.cones.shape[2], device=device, lanes=lanes,
+                   bone_damp=wl.bone_damp)
 
     def info(self) -> dict:
         inf = MbikPlanInfo()

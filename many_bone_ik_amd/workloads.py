@@ -8,7 +8,7 @@ can be regenerated on its own.
 Draw order per skeleton (fixed; changing it changes every fixture):
   1. for every bone b:   L ~ U[0.8, 1.2], axis ~ S^2 (2 draws), angle ~ U[0, 15 deg]
   2. for every bone b:   perturbation axis ~ S^2 (2 draws), angle ~ U[0, 30 deg]
-  3. constrained configs, for every bone b >= 1: helper vector ~ S^2 (2 draws)
+  3. constrained configs, for every parented bone b: helper vector ~ S^2 (2 draws)
 
 Pose layout  [skel][bone][10] = quaternion xyzw | position xyz | scale xyz  (float32)
 Target layout [skel][pin][12] = basis rows r0 r1 r2 | origin            (float32)
@@ -71,13 +71,36 @@ class Workload:
     cones: np.ndarray     # float32 [n][C][max_cones][4]
     twist: np.ndarray     # float32 [n][C][2]
     default_damp: float = math.radians(5.0)
-    pin_weight: float = 1.0
-    pin_priority: tuple[float, float, float] = (0.2, 0.0, 0.2)
-    pin_propagation: float = 1.0
+    pin_weight: np.ndarray | None = None        # [P] float32, default 1.0 (template default is 0)
+    pin_priority: np.ndarray | None = None      # [P][3], default (0.2, 0, 0.2)
+    pin_propagation: np.ndarray | None = None   # [P], default 1.0
+    cone_count: np.ndarray | None = None        # [C] cones per constraint, default topo.cones_per_bone
+    bone_damp: np.ndarray | None = None         # ManyBoneIK3D::bone_damp, default empty
+
+    def __post_init__(self):
+        P = int(self.topo.pins.shape[0])
+        C = int(self.topo.constrained.shape[0])
+        if self.pin_weight is None:
+            self.pin_weight = np.ones(P, np.float32)
+        if self.pin_priority is None:
+            self.pin_priority = np.tile(np.array([0.2, 0.0, 0.2], np.float32), (P, 1))
+        if self.pin_propagation is None:
+            self.pin_propagation = np.ones(P, np.float32)
+        if self.cone_count is None:
+            self.cone_count = np.full(C, self.topo.cones_per_bone, np.int32)
 
     @property
     def bone_count(self) -> int:
         return int(self.topo.parents.shape[0])
+
+    def pins(self) -> list[dict]:
+        return [dict(bone=int(b), weight=float(self.pin_weight[i]),
+                     direction_priorities=tuple(float(x) for x in self.pin_priority[i]),
+                     motion_propagation_factor=float(self.pin_propagation[i]))
+                for i, b in enumerate(self.topo.pins)]
+
+    def constraints(self) -> list[dict]:
+        return [dict(bone=int(b), cone_count=int(self.cone_count[i])) for i, b in enumerate(self.topo.constrained)]
 
 
 def _chain(parents: list[int], start_parent: int, length: int) -> int:
@@ -170,9 +193,16 @@ def _rotate(v: np.ndarray, axis: np.ndarray, angle: float) -> np.ndarray:
     return v * c + np.cross(axis, v) * s + axis * (np.sum(axis * v, -1, keepdims=True)) * (1 - c)
 
 
-def generate(cfg: int, n: int, first: int = 0, seed: int = SEED) -> Workload:
-    """Generate skeletons [first, first+n) of config ``cfg`` (1..5)."""
-    topo = topology(cfg)
+def custom_topology(parents, pins, constrained=(), cones_per_bone=0, twist=None, iterations=16,
+                    name="custom") -> Topology:
+    return Topology(name, np.asarray(parents, np.int32), np.asarray(pins, np.int32),
+                    np.asarray(constrained, np.int32), int(iterations), twist, int(cones_per_bone))
+
+
+def generate(cfg: int, n: int, first: int = 0, seed: int = SEED, topo: Topology | None = None) -> Workload:
+    """Generate skeletons [first, first+n) of config ``cfg`` (1..5), or of ``topo`` (then
+    ``cfg`` only seeds the streams).  Constrained bones must not be parentless."""
+    topo = topology(cfg) if topo is None else topo
     B = topo.parents.shape[0]
     idx = np.arange(first, first + n, dtype=np.uint64)
     rng = SplitMix64(np.uint64(seed) ^ (np.uint64(cfg) << np.uint64(40)) ^ idx)
@@ -187,7 +217,8 @@ def generate(cfg: int, n: int, first: int = 0, seed: int = SEED) -> Workload:
         pert_angle[:, b] = math.radians(30.0) * rng.uniform()
     q_rest = _quat_from_axis_angle(rest_axis, rest_angle)
     pos = np.zeros((n, B, 3))
-    pos[:, 1:, 1] = length[:, 1:]
+    has_parent = topo.parents >= 0
+    pos[:, has_parent, 1] = length[:, has_parent]
     pose = np.zeros((n, B, 10), np.float32)
     pose[..., 0:4] = q_rest
     pose[..., 4:7] = pos
@@ -197,7 +228,19 @@ def generate(cfg: int, n: int, first: int = 0, seed: int = SEED) -> Workload:
     q_pert = _quat_mul(_quat_from_axis_angle(pert_axis, pert_angle), q_rest)
     R = _quat_to_mat(q_pert)
     G_R = np.empty((n, B, 3, 3)); G_o = np.empty((n, B, 3))
+    order, seen = [], set()
+
+    def visit(b):
+        if b in seen:
+            return
+        if topo.parents[b] >= 0:
+            visit(int(topo.parents[b]))
+        seen.add(b)
+        order.append(b)
+
     for b in range(B):
+        visit(b)
+    for b in order:
         p = topo.parents[b]
         if p < 0:
             G_R[:, b] = R[:, b]; G_o[:, b] = pos[:, b]
@@ -214,9 +257,10 @@ def generate(cfg: int, n: int, first: int = 0, seed: int = SEED) -> Workload:
     cones = np.zeros((n, C, mc, 4), np.float32)
     twist = np.zeros((n, C, 2), np.float32)
     if C:
-        helper = np.empty((n, B, 3))
-        for b in range(1, B):
-            helper[:, b] = rng.unit_vector()
+        helper = np.zeros((n, B, 3))
+        for b in range(B):
+            if topo.parents[b] >= 0:
+                helper[:, b] = rng.unit_vector()
         rest_dir = _quat_to_mat(q_rest)[..., :, 1]          # R_local * (0,1,0), parent frame
         cb = topo.constrained
         c0 = rest_dir[:, cb]
@@ -228,8 +272,9 @@ def generate(cfg: int, n: int, first: int = 0, seed: int = SEED) -> Workload:
         if topo.cones_per_bone > 1:
             cones[:, :, 1, 0:3] = c1
             cones[:, :, 1, 3] = math.radians(20.0)
-        twist[..., 0] = topo.twist[0]
-        twist[..., 1] = topo.twist[1]
+        if topo.twist is not None:
+            twist[..., 0] = topo.twist[0]
+            twist[..., 1] = topo.twist[1]
     return Workload(topo, n, pose, targets, cones, twist)
 
 

@@ -1327,6 +1327,57 @@ void oracle_destroy(void *h) {
 	free(o);
 }
 
+/* Post-order segment numbering (children before parents), as the product's plan uses. */
+static void post_order(skel_t *s, int si, int *out, int *n) {
+	segment_t *g = &s->segs[si];
+	for (int i = 0; i < g->nchild; i++) post_order(s, g->childs[i], out, n);
+	out[(*n)++] = si;
+}
+static int seg_by_post_index(skel_t *s, int idx) {
+	int order[4096], n = 0;
+	for (int r = 0; r < s->nroots; r++) post_order(s, s->roots[r], order, &n);
+	return idx >= 0 && idx < n ? order[idx] : -1;
+}
+int32_t oracle_segment_table(void *h, int32_t *root, int32_t *tip, int32_t *nh, int32_t cap) {
+	oracle_t *o = (oracle_t *)h;
+	if (!o->n) return 0;
+	skel_t *s = &o->sk[0];
+	int order[4096], n = 0;
+	for (int r = 0; r < s->nroots; r++) post_order(s, s->roots[r], order, &n);
+	for (int i = 0; i < n && i < cap; i++) {
+		root[i] = s->segs[order[i]].root;
+		tip[i] = s->segs[order[i]].tip;
+		nh[i] = s->segs[order[i]].nh;
+	}
+	return n;
+}
+/* One IKBoneSegment3D::segment_solver() call (ik_bone_segment_3d.cpp:210-225) on segment
+ * `post_index` for skeletons [first, first+count); pose_inout is updated in place. */
+int32_t oracle_segment_solve(void *h, int32_t post_index, int32_t first, int32_t count, float *pose_inout, const float *targets) {
+	oracle_t *o = (oracle_t *)h;
+	const oracle_desc *d = &o->desc;
+	int B = d->bone_count, P = d->pin_count;
+	if (first < 0 || count < 0 || first + count > o->n) return -1;
+	for (int i = 0; i < count; i++) {
+		skel_t *s = &o->sk[first + i];
+		int si = seg_by_post_index(s, post_index);
+		if (si < 0) return -1;
+		int maxh = 0;
+		for (int g = 0; g < s->nsegs; g++)
+			if (s->segs[g].nh > maxh) maxh = s->segs[g].nh;
+		v3 *scratch = (v3 *)xcalloc(2 * maxh + 2, sizeof(v3));
+		float *pose = pose_inout + (size_t)i * B * 10;
+		update_ik_bones_transform(s, pose, targets + (size_t)i * P * 12);
+		seg_solver(s, si, d->bone_damp, d->bone_damp_count, d->default_damp, d->constraint_mode, scratch);
+		for (int k = s->nbone_list; k-- > 0;) {
+			int bi = s->bone_list[k];
+			write_pose(&s->nodes[s->bones[bi].pose].local, pose + 10 * bi);
+		}
+		free(scratch);
+	}
+	return 0;
+}
+
 int32_t oracle_segment_count(void *h) {
 	oracle_t *o = (oracle_t *)h;
 	return o->n ? o->sk[0].nsegs : 0;

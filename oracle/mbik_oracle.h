@@ -59,6 +59,11 @@ void oracle_destroy(void *h);
 /* Introspection for tests: segment/effector structure of skeleton 0. */
 int32_t oracle_segment_count(void *h);
 int32_t oracle_bone_list(void *h, int32_t *out_bone_ids, int32_t cap);
+/* Post-order (children first) segment table of skeleton 0: root bone, tip bone, headings. */
+int32_t oracle_segment_table(void *h, int32_t *root, int32_t *tip, int32_t *nh, int32_t cap);
+/* One segment_solver() call on segment `post_index` (post-order numbering), in place. */
+int32_t oracle_segment_solve(void *h, int32_t post_index, int32_t first, int32_t count, float *pose_inout,
+		const float *targets);
 
 /* Unit entry points mirroring the reference's own KATs. */
 /* QCP::weighted_superpose (qcp.cpp:220) + get_translation (qcp.cpp:135). */

@@ -53,6 +53,10 @@ def lib():
         L.oracle_segment_count.restype = C.c_int32
         L.oracle_bone_list.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
         L.oracle_bone_list.restype = C.c_int32
+        L.oracle_segment_table.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32]
+        L.oracle_segment_table.restype = C.c_int32
+        L.oracle_segment_solve.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]
+        L.oracle_segment_solve.restype = C.c_int32
         L.oracle_qcp.argtypes = [_f32p, _f32p, _f64p, C.c_int32, C.c_int32, C.c_double, _f32p, _f32p]
         L.oracle_local_point_in_limits.restype = C.c_double
         L.oracle_local_point_in_limits.argtypes = [_f32p, C.c_int32, C.c_void_p, _f32p, _f32p]
@@ -91,17 +95,20 @@ class Oracle:
         d.parents = _ptr(keep(t.parents, np.int32))
         d.pin_count = P
         d.pin_bone = _ptr(keep(t.pins, np.int32))
-        d.pin_weight = _ptr(keep(np.full(P, wl.pin_weight), np.float32))
-        d.pin_priority = _ptr(keep(np.tile(np.array(wl.pin_priority, np.float32), (P, 1)), np.float32))
-        d.pin_propagation = _ptr(keep(np.full(P, wl.pin_propagation), np.float32))
+        d.pin_weight = _ptr(keep(np.broadcast_to(np.asarray(wl.pin_weight, np.float32), (P,)), np.float32))
+        d.pin_priority = _ptr(keep(np.broadcast_to(np.asarray(wl.pin_priority, np.float32), (P, 3)), np.float32))
+        d.pin_propagation = _ptr(keep(np.broadcast_to(np.asarray(wl.pin_propagation, np.float32), (P,)), np.float32))
         d.constraint_count = Cn
         d.constraint_bone = _ptr(keep(t.constrained, np.int32))
-        d.constraint_cone_count = _ptr(keep(np.full(Cn, t.cones_per_bone), np.int32))
+        cc = getattr(wl, "cone_count", None)
+        d.constraint_cone_count = _ptr(keep(np.full(Cn, t.cones_per_bone) if cc is None else cc, np.int32))
         d.max_cones = wl.cones.shape[2]
         d.iterations = t.iterations if iterations is None else iterations
         d.default_damp = wl.default_damp if default_damp is None else default_damp
         d.constraint_mode = int(constraint_mode)
         d.stabilization_passes = stabilization_passes
+        if bone_damp is None:
+            bone_damp = getattr(wl, "bone_damp", None)
         bd = keep(np.zeros(0) if bone_damp is None else bone_damp, np.float32)
         d.bone_damp_count = bd.shape[0]
         d.bone_damp = _ptr(bd) if bd.shape[0] else None
@@ -135,6 +142,20 @@ class Oracle:
         buf = np.zeros(self.B, np.int32)
         n = lib().oracle_bone_list(self.h, _ptr(buf), self.B)
         return buf[:n].tolist()
+
+    def segment_table(self):
+        cap = self.B
+        r = np.zeros(cap, np.int32); t = np.zeros(cap, np.int32); nh = np.zeros(cap, np.int32)
+        n = lib().oracle_segment_table(self.h, _ptr(r), _ptr(t), _ptr(nh), cap)
+        return r[:n], t[:n], nh[:n]
+
+    def segment_solve(self, post_index, pose, targets, first=0):
+        pose = np.ascontiguousarray(pose, np.float32).copy()
+        targets = np.ascontiguousarray(targets, np.float32)
+        rc = lib().oracle_segment_solve(self.h, post_index, first, pose.shape[0], _ptr(pose), _ptr(targets))
+        if rc != 0:
+            raise RuntimeError("oracle_segment_solve failed")
+        return pose
 
     def close(self):
         if self.h:

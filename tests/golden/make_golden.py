@@ -1,0 +1,52 @@
+"""Regenerates the committed oracle fixtures in tests/golden/ (run from the repo root):
+
+    python tests/golden/make_golden.py
+
+Each fixture stores the generator coordinates (config, first skeleton, count), a SHA-256
+of the generated inputs (so generator drift is caught), and the oracle's outputs:
+full-frame poses, and for C1 (the reference's own CPU case) the pose after every
+iteration.  The oracle is the plain-C restatement in oracle/ (transcendentals pinned to
+correctly rounded evaluation, see oracle/godot_math.h).
+"""
+from __future__ import annotations
+
+import hashlib
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+from many_bone_ik_amd import workloads as W  # noqa: E402
+from oracle import pyoracle as po  # noqa: E402
+
+FIXTURES = [(1, 0, 1), (2, 0, 4), (3, 0, 4), (4, 0, 2), (5, 0, 1), (2, 4093, 3)]
+
+
+def input_digest(wl) -> str:
+    h = hashlib.sha256()
+    for a in (wl.pose, wl.targets, wl.cones, wl.twist):
+        h.update(np.ascontiguousarray(a).tobytes())
+    return h.hexdigest()
+
+
+def main():
+    for cfg, first, n in FIXTURES:
+        wl = W.generate(cfg, n, first=first)
+        o = po.Oracle(wl)
+        out, trace = o.solve(wl.pose, wl.targets, trace=True)
+        seg_root, seg_tip, seg_nh = o.segment_table()
+        # one segment_solver() call on the first (deepest) segment, from the input pose
+        seg0 = o.segment_solve(0, wl.pose, wl.targets)
+        name = os.path.join(HERE, f"oracle_c{cfg}_{first}_{n}.npz")
+        np.savez_compressed(name, cfg=cfg, first=first, n=n, digest=input_digest(wl), pose_out=out,
+                            trace=trace if cfg == 1 else trace[:, :1], seg_root=seg_root, seg_tip=seg_tip,
+                            seg_nh=seg_nh, bone_list=np.array(o.bone_list(), np.int32), segment0_pose=seg0)
+        print(name, os.path.getsize(name), "bytes")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,106 @@
+"""Edge cases the reference's code paths have, GPU vs oracle, bitwise."""
+import math
+
+import numpy as np
+import pytest
+
+from many_bone_ik_amd import workloads as W
+from many_bone_ik_amd.ik import ManyBoneIK3D
+from many_bone_ik_amd.solver import Plan
+from tests.test_gpu_parity import assert_parity
+
+pytestmark = pytest.mark.gpu
+
+
+def run(oracle, wl, **kw):
+    ref = oracle.Oracle(wl, **kw).solve(wl.pose, wl.targets)
+    got = Plan.from_workload(wl, **{k: v for k, v in kw.items() if k in ("iterations",)}).solve_host(wl.pose, wl.targets)
+    return got, ref
+
+
+def with_pins(wl, **arrays):
+    for k, v in arrays.items():
+        setattr(wl, k, np.asarray(v, np.float32))
+    return wl
+
+
+CASES = {
+    # name: (parents, pins, constrained, cones_per_bone, twist)
+    "dropped_branch": ([-1, 0, 1, 1, 3, 0, 5, 6], [2, 7], [1, 2, 5, 6, 7], 2, (0.2, 1.5)),
+    "multi_root_released_origin": ([-1, 0, 1, -1, 3, 4], [2, 5], [1, 2, 4, 5], 1, (-0.3, 2.0)),
+    "pinned_root": ([-1, 0, 1, 0, 3], [0, 2, 4], [1, 2, 3, 4], 2, (0.0, math.tau)),
+    "mid_chain_pin": ([-1, 0, 1, 2, 3, 4], [2, 5], [1, 2, 3, 4, 5], 2, (0.1, 0.5)),
+    "unsorted_parents": ([2, 2, -1, 1, 0], [3, 4], [0, 1, 3, 4], 2, (0.0, 1.0)),
+    "three_cones": ([-1, 0, 1, 2, 0, 4, 5], [3, 6], [1, 2, 3, 4, 5, 6], 3, (0.0, 1.0)),
+    "zero_cones": ([-1, 0, 1, 2, 0, 4, 5], [3, 6], [1, 2, 3, 4, 5, 6], 0, (0.0, 0.3)),
+    "tight_twist": ([-1, 0, 1, 2, 3, 0, 5, 6], [4, 7], [1, 2, 3, 4, 5, 6, 7], 1, (math.radians(-5), math.radians(10))),
+    "wide_fan_17_effectors": ([-1] + [0] * 17 + list(range(1, 18)), list(range(18, 35)), [], 0, None),
+}
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_topology_edge_cases(oracle, mbik, name):
+    parents, pins, cons, ncones, twist = CASES[name]
+    topo = W.custom_topology(parents, pins, cons, cones_per_bone=ncones, twist=twist)
+    wl = W.generate(11, 16, topo=topo)
+    got, ref = run(oracle, wl)
+    assert_parity(got, ref, name)
+
+
+@pytest.mark.parametrize("variant", ["all_axes", "no_axes", "zero_weight", "propagation_zero", "propagation_half",
+                                     "mixed_weights", "bone_damp"])
+def test_pin_and_damp_variants(oracle, mbik, variant):
+    wl = W.generate(2, 12)
+    P = wl.topo.pins.shape[0]
+    if variant == "all_axes":
+        with_pins(wl, pin_priority=np.tile([0.3, 0.5, 0.1], (P, 1)))
+    elif variant == "no_axes":                     # one heading per effector, single-pair QCP
+        with_pins(wl, pin_priority=np.zeros((P, 3)))
+    elif variant == "zero_weight":                 # template default: QCP sums vanish -> identity
+        with_pins(wl, pin_weight=np.zeros(P))
+    elif variant == "propagation_zero":
+        with_pins(wl, pin_propagation=np.zeros(P))
+    elif variant == "propagation_half":
+        with_pins(wl, pin_propagation=np.full(P, 0.5))
+    elif variant == "mixed_weights":
+        with_pins(wl, pin_weight=np.array([1.0, 0.25, 3.0, 0.0]))
+    elif variant == "bone_damp":
+        wl.bone_damp = np.linspace(0.01, 0.2, 40).astype(np.float32)
+    got, ref = run(oracle, wl)
+    assert_parity(got, ref, variant)
+
+
+def test_single_heading_root_segment(oracle, mbik):
+    """Chain whose root segment holds one heading: QCP's single-pair branch with translate."""
+    topo = W.custom_topology([-1, 0, 1, 2], [3], [], iterations=8)
+    wl = W.generate(12, 8, topo=topo)
+    with_pins(wl, pin_priority=np.zeros((1, 3)))
+    got, ref = run(oracle, wl)
+    assert_parity(got, ref, "single heading")
+
+
+def test_no_pins_leaves_poses(oracle, mbik):
+    topo = W.custom_topology([-1, 0, 1], [], [])
+    wl = W.generate(13, 4, topo=topo)
+    got, ref = run(oracle, wl)
+    assert np.array_equal(got, wl.pose) and np.array_equal(ref, wl.pose)
+
+
+def test_host_api_mirror_end_to_end(oracle, mbik):
+    """ManyBoneIK3D mirror configured like a Godot scene, solved on the GPU, vs the oracle."""
+    wl = W.generate(2, 8)
+    parents = wl.topo.parents
+    ik = ManyBoneIK3D(parents)
+    ik.set_iterations_per_frame(16)
+    ik.set_total_effector_count(4)
+    for i, b in enumerate(wl.topo.pins):
+        ik.set_effector_bone_name(i, f"bone_{b}")
+        ik.set_pin_weight(i, 1.0)
+    ik._set_constraint_count(len(wl.topo.constrained))
+    for i, b in enumerate(wl.topo.constrained):
+        ik.set_constraint_name_at_index(i, f"bone_{b}")
+        ik.set_kusudama_open_cone_count(i, 2)
+        ik.set_joint_twist(i, (0.0, math.tau))
+    got = ik.process_modification(wl.pose, wl.targets, cones=wl.cones, twist=wl.twist)
+    ref = oracle.Oracle(wl).solve(wl.pose, wl.targets)
+    assert_parity(got, ref, "ManyBoneIK3D mirror")
