@@ -9,7 +9,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmbik.so")
+LIB_PATH = os.environ.get("MBIK_LIB_OVERRIDE") or os.path.join(_HERE, "libmbik.so")  # override: ablation timing only
 
 MBIK_OK = 0
 MBIK_EINVAL = -1

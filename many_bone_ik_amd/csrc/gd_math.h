@@ -27,9 +27,15 @@ constexpr double PI = 3.1415926535897932384626433833;
 // platform libm (Math::sin(float) -> sinf); its dynamics amplify 1-ulp libm differences
 // ~2x per iteration, so the product and the oracle pin the same (correctly rounded,
 // barring rare double-rounding cases) result instead of OCML's own float versions.
+#ifdef MBIK_ABLATE_TRIG
+GDI float sin_f(float x) { return sinf(x); }
+GDI float cos_f(float x) { return cosf(x); }
+GDI float acos_f(float x) { return acosf(x); }
+#else
 GDI float sin_f(float x) { return (float)sin((double)x); }
 GDI float cos_f(float x) { return (float)cos((double)x); }
 GDI float acos_f(float x) { return (float)acos((double)x); }
+#endif
 
 struct V3 {
 	float x, y, z;

@@ -559,6 +559,19 @@ std::string build_skeletons(HostPlan &p, int32_t n, const float *setup_pose, con
 // ---------------------------------------------------------------------------------------
 int32_t lds_floats_per_skeleton(const HostPlan &p) { return p.B * 24 + p.P * 25; }
 
+// Upper bound of the LDS bytes taken by the topology blob (solve.hip: upload_topology).
+int64_t topology_bytes(const HostPlan &p) {
+	int64_t w = 4 * (int64_t)p.sched.size() + 4;
+	auto ints = [&](size_t n) { w += (int64_t)std::max<size_t>(n, 1) + 1; };
+	ints(p.bone_pose_parent.size()); ints(p.bone_depth.size()); ints(p.bone_flags.size()); ints(p.bone_pin.size());
+	ints(p.bone_cons.size()); ints(p.bone_child_eff_off.size()); ints(p.bone_child_effs.size());
+	ints(p.seg_bone_off.size()); ints(p.seg_bones.size()); ints(p.seg_eff_off.size()); ints(p.seg_effs.size());
+	ints(p.seg_eff_hoff.size()); ints(p.seg_nh.size()); ints(p.seg_flags.size()); ints(p.seg_hw_off.size());
+	ints(p.eff_bone.size()); ints(p.eff_path_off.size()); ints(p.eff_path.size()); ints(p.eff_prio.size());
+	ints(p.cons_ncones.size()); ints(2 * p.seg_hw.size()); ints(2 * p.seg_cos_half_damp.size());
+	return (w + 4) * 4;
+}
+
 static int ceil_log2(int v) {
 	int l = 0;
 	while ((1 << l) < v) l++;
@@ -585,8 +598,6 @@ void build_schedule(HostPlan &p, int32_t lanes, int64_t nlaunch) {
 	K = std::max(1, std::min(64, K));
 	p.K = K;
 	p.log2K = ceil_log2(K);
-	p.spw = 64 / K;
-	while (p.spw > 1 && (int64_t)p.spw * ((lds_floats_per_skeleton(p) + 3) & ~3) * 4 > 160 * 1024) p.spw /= 2;
 	p.sched.clear();
 	p.nrows = 0;
 	for (auto &l : lev) {
@@ -600,6 +611,9 @@ void build_schedule(HostPlan &p, int32_t lanes, int64_t nlaunch) {
 			p.nrows++;
 		}
 	}
+	p.spw = 64 / K;
+	const int64_t topo = topology_bytes(p);
+	while (p.spw > 1 && (int64_t)p.spw * ((lds_floats_per_skeleton(p) + 3) & ~3) * 4 + topo > 160 * 1024) p.spw /= 2;
 }
 
 } // namespace mbik

@@ -94,5 +94,6 @@ std::string build_skeletons(HostPlan &plan, int32_t n, const float *setup_pose, 
 void build_schedule(HostPlan &plan, int32_t lanes_per_skeleton, int64_t skeletons_in_launch);
 // LDS floats per skeleton used by the kernel.
 int32_t lds_floats_per_skeleton(const HostPlan &plan);
+int64_t topology_bytes(const HostPlan &plan);
 
 } // namespace mbik

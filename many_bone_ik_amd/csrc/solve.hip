@@ -35,18 +35,41 @@
 
 using namespace gd;
 
+// Diagnostic cycle accounting (-DMBIK_PROF builds only; tools/prof_phases.py reads it):
+// 0 load, 1 headings+QCP, 2 clamp/slerp/rotate, 3 swing, 4 twist, 5 global pass, 6 store, 7 total.
+#ifdef MBIK_PROF
+__device__ unsigned long long g_mbik_prof[8];
+#define MBIK_PROF_PARAM , uint64_t *pf
+#define MBIK_PROF_ARG , pf
+#define MBIK_PROF_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define MBIK_PROF_ADD(i, a, b) pf[i] += (b) - (a)
+#else
+#define MBIK_PROF_PARAM
+#define MBIK_PROF_ARG
+#define MBIK_PROF_T(v)
+#define MBIK_PROF_ADD(i, a, b)
+#endif
+
 namespace {
+
+// Topology tables (shared by every skeleton of the plan).  They are packed into one blob
+// in HBM and copied into LDS at kernel start, so the many small dependent lookups of a
+// bone-step (segment -> effector -> path -> bone) are LDS reads, not L2 round trips.
+#define MBIK_TOPO_TABLES(X)                                                                         \
+	X(int, bone_pose_parent) X(int, bone_depth) X(int, bone_flags) X(int, bone_pin) X(int, bone_cons)  \
+	X(int, bone_child_eff_off) X(int, bone_child_effs) X(int, seg_bone_off) X(int, seg_bones)         \
+	X(int, seg_eff_off) X(int, seg_effs) X(int, seg_eff_hoff) X(int, seg_nh) X(int, seg_flags)         \
+	X(int, seg_hw_off) X(int, eff_bone) X(int, eff_path_off) X(int, eff_path) X(float, eff_prio)       \
+	X(int, cons_ncones) X(double, seg_hw) X(double, seg_cos_half_damp) X(int4, sched)
 
 struct DevPlan {
 	int B, P, NS, NC, max_cones, nrows, K, log2K, spw, lds_stride;
 	int N, cf_stride, cd_stride;
-	const int *bone_pose_parent, *bone_depth, *bone_flags, *bone_pin, *bone_cons, *bone_child_eff_off, *bone_child_effs;
-	const int *seg_bone_off, *seg_bones, *seg_eff_off, *seg_effs, *seg_eff_hoff, *seg_nh, *seg_flags, *seg_hw_off;
-	const double *seg_hw, *seg_cos_half_damp;
-	const int *eff_bone, *eff_path_off, *eff_path;
-	const float *eff_prio;
-	const int4 *sched;
-	const int *cons_ncones;
+	int topo_words; // blob size in 32-bit words (multiple of 4)
+	const uint4 *topo_blob;
+#define MBIK_DECL(T, name) const T *name; int o_##name;
+	MBIK_TOPO_TABLES(MBIK_DECL)
+#undef MBIK_DECL
 	const float *D, *CF;
 	const double *CD;
 };
@@ -354,7 +377,8 @@ __device__ __forceinline__ void swing_twist_y(Q rot, Q &swing, Q &twist) {
 // (ik_bone_segment_3d.cpp:90-181) with stabilization_passes == 0, constraint_mode false.
 // ------------------------------------------------------------------------------------
 __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, size_t s, float *L, const float *G, const float *TG,
-		float *ST, int *SF) {
+		float *ST, int *SF MBIK_PROF_PARAM) {
+	MBIK_PROF_T(pt0);
 	const int b = t.seg_bones[k];
 	const int pp = t.bone_pose_parent[b];
 	const bool hasP = pp != mbik::POSE_PARENT_NONE;
@@ -462,33 +486,48 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, size_t
 		qrot = qcp_adjugate(S);
 	}
 
+	MBIK_PROF_T(pt1);
+	MBIK_PROF_ADD(1, pt0, pt1);
 	// ---- damp clamp, slerp(…, 0), rotate, translate, set_global_pose (:144-154) ----
 	const double chd = t.seg_cos_half_damp[k];
+#ifdef MBIK_ABLATE_CONVERT
+	B3 rot = from_quat(qrot);
+#else
 	B3 rot = from_quat(clamp_cos_half(get_rotation_quaternion(from_quat(qrot)), chd));
+#endif
+#ifndef MBIK_ABLATE_SLERP
 	rot = slerp_weight0(rot, Gb.b);
+#endif
 	const B3 Pinv = inverse(P.b);
 	if (hasP) Lb.b = ((Pinv * rot) * P.b) * Lb.b;
 	X3 Gn = hasP ? P * Lb : Lb;
 	X3 result = {Gn.b, Gn.o + translation};
-	Lb = hasP ? affine_inverse(P) * result : result;
+	// affine_inverse(P) with P.basis.inverse() already at hand (same arithmetic)
+	Lb = hasP ? X3{Pinv, xform(Pinv, -P.o)} * result : result;
 	// set_global_pose propagates through b's subtree: pinned children's stale
 	// bone-direction caches are refreshed from here on.
 	// Every lane of the group holds identical values, so each writes its own copy (same
 	// bytes) and later reads never depend on another lane's store ordering.
 	for (int c = t.bone_child_eff_off[b]; c < t.bone_child_eff_off[b + 1]; c++) SF[t.bone_child_effs[c]] = 0;
 
+	MBIK_PROF_T(pt2);
+	MBIK_PROF_ADD(2, pt1, pt2);
 	// ---- Kusudama: orientation (swing) snap (ik_kusudama_3d.cpp:347-376) ----
 	const int flags = t.bone_flags[b];
 	bool swung = false;
 	X3 Gbd_stale;
+#ifdef MBIK_ABLATE_SWING
+	if (false) {
+#else
 	if (flags & mbik::BF_ORIENT) {
+#endif
 		const int slot = t.bone_cons[b];
 		X3 Gs = P * Lb;
 		Gbd_stale.b = Gs.b * ld_soa_basis(t.D, b, 9, 0, t.N, s);
 		Gbd_stale.o = Gs.o;
 		X3 Gco = {P.b, xform(P, Lb.o)}; // constraint_orientation: (I, pose local origin) under the parent
 		V3 bdx = xform(Gbd_stale, v3(0.0f, 1.0f, 0.0f));
-		V3 tip = xform(affine_inverse(Gco), bdx);
+		V3 tip = xform(X3{Pinv, xform(Pinv, -Gco.o)}, bdx); // Gco.basis == P.basis
 		double in_bounds = 1.0;
 		V3 inl = local_point_in_limits(t, slot, s, tip, in_bounds);
 		if (in_bounds < 0) {
@@ -498,9 +537,15 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, size_t
 			swung = true;
 		}
 	}
+	MBIK_PROF_T(pt3);
+	MBIK_PROF_ADD(3, pt2, pt3);
 	// ---- Kusudama: twist snap (ik_kusudama_3d.cpp:117-132) ----
 	bool twist_changed = false;
+#ifdef MBIK_ABLATE_TWIST
+	if (false) {
+#else
 	if (flags & mbik::BF_AXIAL) {
+#endif
 		const int slot = t.bone_cons[b];
 		const int cs = t.cf_stride;
 		Q tcr = q4(soa(t.CF, slot, cs, mbik::CF_TWIST_Q, t.N, s), soa(t.CF, slot, cs, mbik::CF_TWIST_Q + 1, t.N, s),
@@ -529,6 +574,8 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, size_t
 			SF[e] = 1;
 		}
 	}
+	MBIK_PROF_T(pt4);
+	MBIK_PROF_ADD(4, pt3, pt4);
 }
 
 // Iteration-start globals of one segment, root -> tip (IKNode3D::get_global_transform).
@@ -556,8 +603,21 @@ __device__ void write_pose(const X3 &t, float *out) {
 __global__ __launch_bounds__(64) void mbik_solve_kernel(DevPlan t, int first, int count, const float *__restrict__ pose_in,
 		const float *__restrict__ targets, float *__restrict__ pose_out, int iterations, int seg_lo, int seg_hi) {
 	extern __shared__ float4 lds4[];
-	float *lds = reinterpret_cast<float *>(lds4);
 	const int lane = threadIdx.x;
+#ifdef MBIK_PROF
+	uint64_t pfa[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+	uint64_t *pf = pfa;
+#endif
+	MBIK_PROF_T(pk0);
+	{
+		uint4 *dst = reinterpret_cast<uint4 *>(lds4);
+		for (int i = lane; i < (t.topo_words >> 2); i += 64) dst[i] = t.topo_blob[i];
+	}
+	const uint32_t *topo = reinterpret_cast<const uint32_t *>(lds4);
+#define MBIK_REPOINT(T, name) t.name = reinterpret_cast<const T *>(topo + t.o_##name);
+	MBIK_TOPO_TABLES(MBIK_REPOINT)
+#undef MBIK_REPOINT
+	float *lds = reinterpret_cast<float *>(lds4) + t.topo_words;
 	const int g = lane >> t.log2K;
 	const int role = lane & (t.K - 1);
 	const int local = blockIdx.x * t.spw + g;
@@ -579,21 +639,27 @@ __global__ __launch_bounds__(64) void mbik_solve_kernel(DevPlan t, int first, in
 		}
 	}
 	__syncthreads();
+	MBIK_PROF_T(pk1);
+	MBIK_PROF_ADD(0, pk0, pk1);
 	for (int it = 0; it < iterations; it++) {
+		MBIK_PROF_T(pg0);
 		for (int r = t.nrows - 1; r >= 0; r--) {
 			const int4 task = t.sched[r * K + role];
 			if (valid && task.x >= 0 && task.y == 0) global_pass(t, task.x, L, G);
 			__syncthreads();
 		}
+		MBIK_PROF_T(pg1);
+		MBIK_PROF_ADD(5, pg0, pg1);
 		for (int r = 0; r < t.nrows; r++) {
 			const int4 task = t.sched[r * K + role];
 			if (valid && task.x >= seg_lo && task.x <= seg_hi) {
 				for (int k = t.seg_bone_off[task.x]; k < t.seg_bone_off[task.x + 1]; k++)
-					bone_step(t, task.x, k, task.y, task.z, s, L, G, TG, ST, SF);
+					bone_step(t, task.x, k, task.y, task.z, s, L, G, TG, ST, SF MBIK_PROF_ARG);
 			}
 			__syncthreads();
 		}
 	}
+	MBIK_PROF_T(pk2);
 	if (valid) {
 		for (int b = role; b < B; b += K) {
 			float *dst = pose_out + ((size_t)local * B + b) * 10;
@@ -605,6 +671,13 @@ __global__ __launch_bounds__(64) void mbik_solve_kernel(DevPlan t, int first, in
 			}
 		}
 	}
+	MBIK_PROF_T(pk3);
+	MBIK_PROF_ADD(6, pk2, pk3);
+	MBIK_PROF_ADD(7, pk0, pk3);
+#ifdef MBIK_PROF
+	if (lane == 0)
+		for (int i = 0; i < 8; i++) atomicAdd(&g_mbik_prof[i], (unsigned long long)pfa[i]);
+#endif
 }
 
 } // namespace
@@ -621,7 +694,7 @@ struct mbik_plan {
 	int64_t device_bytes = 0;
 	double alg_bytes = 0;
 	int sched_K = -1;
-	int4 *d_sched = nullptr;
+	void *d_sched = nullptr; // topology blob (includes the lane schedule)
 	// scratch for mbik_solve_host
 	float *d_in = nullptr, *d_tg = nullptr, *d_out = nullptr;
 	size_t scratch_skel = 0;
@@ -659,20 +732,43 @@ int upload(mbik_plan *p, const std::vector<T> &v, const T *&dst) {
 	return MBIK_OK;
 }
 
+// Packs the topology tables (and the schedule for the current lane count) into one blob.
+int upload_topology(mbik_plan *p) {
+	const mbik::HostPlan &h = p->host;
+	DevPlan &d = p->dev;
+	std::vector<uint32_t> blob;
+	auto add = [&](const void *data, size_t bytes, size_t align_words, int &off) {
+		while (blob.size() % align_words) blob.push_back(0);
+		off = (int)blob.size();
+		size_t w = (bytes + 3) / 4;
+		blob.resize(blob.size() + std::max<size_t>(w, 1), 0);
+		if (bytes) std::memcpy(blob.data() + off, data, bytes);
+	};
+	std::vector<int4> rows(h.sched.size());
+	for (size_t i = 0; i < rows.size(); i++) rows[i] = make_int4(h.sched[i].seg, h.sched[i].j, h.sched[i].m, 0);
+	add(rows.data(), rows.size() * sizeof(int4), 4, d.o_sched);
+#define MBIK_ADD(T, name) \
+	if (std::string(#name) != "sched") add(h.name.data(), h.name.size() * sizeof(h.name[0]), sizeof(T) >= 8 ? 2 : 1, d.o_##name);
+	MBIK_TOPO_TABLES(MBIK_ADD)
+#undef MBIK_ADD
+	while (blob.size() % 4) blob.push_back(0);
+	if (p->d_sched) (void)hipFree(p->d_sched);
+	p->d_sched = nullptr;
+	if (hipMalloc(&p->d_sched, blob.size() * 4) != hipSuccess) return fail(MBIK_ENOMEM, "hipMalloc topology blob");
+	if (hipMemcpy(p->d_sched, blob.data(), blob.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+		return fail(MBIK_EHIP, "hipMemcpy topology blob");
+	d.topo_blob = reinterpret_cast<const uint4 *>(p->d_sched);
+	d.topo_words = (int)blob.size();
+	return MBIK_OK;
+}
+
 int ensure_schedule(mbik_plan *p, int64_t nlaunch) {
 	mbik::HostPlan &h = p->host;
 	mbik::build_schedule(h, p->lanes_override, nlaunch);
 	if (p->sched_K == h.K && p->d_sched) return MBIK_OK;
-	if (p->d_sched) (void)hipFree(p->d_sched);
-	p->d_sched = nullptr;
-	std::vector<int4> rows(h.sched.size());
-	for (size_t i = 0; i < rows.size(); i++) rows[i] = make_int4(h.sched[i].seg, h.sched[i].j, h.sched[i].m, 0);
-	if (rows.empty()) rows.push_back(make_int4(-1, 0, 1, 0));
-	if (hipMalloc(&p->d_sched, rows.size() * sizeof(int4)) != hipSuccess) return fail(MBIK_ENOMEM, "hipMalloc sched");
-	if (hipMemcpy(p->d_sched, rows.data(), rows.size() * sizeof(int4), hipMemcpyHostToDevice) != hipSuccess)
-		return fail(MBIK_EHIP, "hipMemcpy sched");
+	int rc = upload_topology(p);
+	if (rc) return rc;
 	p->sched_K = h.K;
-	p->dev.sched = p->d_sched;
 	p->dev.nrows = h.nrows;
 	p->dev.K = h.K;
 	p->dev.log2K = h.log2K;
@@ -696,7 +792,7 @@ int launch(mbik_plan *p, int first, int count, const float *pose_in, const float
 	}
 	int rc = ensure_schedule(p, count);
 	if (rc) return rc;
-	size_t lds = (size_t)h.spw * p->dev.lds_stride * sizeof(float);
+	size_t lds = ((size_t)h.spw * p->dev.lds_stride + p->dev.topo_words) * sizeof(float);
 	if (lds > 160 * 1024) return fail(MBIK_EUNSUPPORTED, "skeleton too large for LDS at this lane count");
 	static std::once_flag once;
 	std::call_once(once, [] { (void)hipFuncSetAttribute((const void *)mbik_solve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); });
@@ -758,28 +854,6 @@ int32_t mbik_plan_create(const mbik_skeleton_desc *desc, const mbik_config *conf
 	d.cf_stride = h.cf_stride(); d.cd_stride = h.cd_stride();
 	d.lds_stride = (mbik::lds_floats_per_skeleton(h) + 3) & ~3;
 	int rc = 0;
-	rc = rc ? rc : upload(p.get(), h.bone_pose_parent, d.bone_pose_parent);
-	rc = rc ? rc : upload(p.get(), h.bone_depth, d.bone_depth);
-	rc = rc ? rc : upload(p.get(), h.bone_flags, d.bone_flags);
-	rc = rc ? rc : upload(p.get(), h.bone_pin, d.bone_pin);
-	rc = rc ? rc : upload(p.get(), h.bone_cons, d.bone_cons);
-	rc = rc ? rc : upload(p.get(), h.bone_child_eff_off, d.bone_child_eff_off);
-	rc = rc ? rc : upload(p.get(), h.bone_child_effs, d.bone_child_effs);
-	rc = rc ? rc : upload(p.get(), h.seg_bone_off, d.seg_bone_off);
-	rc = rc ? rc : upload(p.get(), h.seg_bones, d.seg_bones);
-	rc = rc ? rc : upload(p.get(), h.seg_eff_off, d.seg_eff_off);
-	rc = rc ? rc : upload(p.get(), h.seg_effs, d.seg_effs);
-	rc = rc ? rc : upload(p.get(), h.seg_eff_hoff, d.seg_eff_hoff);
-	rc = rc ? rc : upload(p.get(), h.seg_nh, d.seg_nh);
-	rc = rc ? rc : upload(p.get(), h.seg_flags, d.seg_flags);
-	rc = rc ? rc : upload(p.get(), h.seg_hw_off, d.seg_hw_off);
-	rc = rc ? rc : upload(p.get(), h.seg_hw, d.seg_hw);
-	rc = rc ? rc : upload(p.get(), h.seg_cos_half_damp, d.seg_cos_half_damp);
-	rc = rc ? rc : upload(p.get(), h.eff_bone, d.eff_bone);
-	rc = rc ? rc : upload(p.get(), h.eff_path_off, d.eff_path_off);
-	rc = rc ? rc : upload(p.get(), h.eff_path, d.eff_path);
-	rc = rc ? rc : upload(p.get(), h.eff_prio, d.eff_prio);
-	rc = rc ? rc : upload(p.get(), h.cons_ncones, d.cons_ncones);
 	rc = rc ? rc : upload(p.get(), h.D, d.D);
 	rc = rc ? rc : upload(p.get(), h.CF, d.CF);
 	rc = rc ? rc : upload(p.get(), h.CD, d.CD);
@@ -896,3 +970,11 @@ int32_t mbik_solve_host(mbik_plan *p, int32_t first, int32_t count, const float 
 }
 
 } // extern "C"
+
+#ifdef MBIK_PROF
+extern "C" int mbik_debug_prof(unsigned long long *out) {
+	if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mbik_prof), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
+	unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+	return hipMemcpyToSymbol(HIP_SYMBOL(g_mbik_prof), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -1,0 +1,5 @@
+#!/bin/bash
+for tag in BASE CONVERT SLERP SWING TWIST; do
+  if [ $tag = BASE ]; then unset MBIK_LIB_OVERRIDE; else export MBIK_LIB_OVERRIDE=$PWD/build/abl/libmbik_abl_$tag.so; fi
+  echo "== $tag"; timeout -k 10 200 python tools/sweep.py 2:4096:16:4 3:65536:8 2>/dev/null
+done

@@ -1,0 +1,32 @@
+"""Per-phase cycle accounting of the solve kernel (needs a -DMBIK_PROF build named by
+MBIK_LIB_OVERRIDE, see tools/prof_build.sh).  Prints, per config, the share of wave
+cycles spent in each phase (summed over waves; one solve launch)."""
+import ctypes as C, json, sys
+import torch
+sys.path.insert(0, '.')
+from many_bone_ik_amd import _lib, workloads as W
+from many_bone_ik_amd.solver import Plan
+
+NAMES = ["load", "headings_qcp", "clamp_slerp_rotate", "swing", "twist", "global_pass", "store", "total"]
+dev = torch.device('cuda', 0)
+L = _lib.load()
+L.mbik_debug_prof.argtypes = [C.c_void_p]
+buf = (C.c_ulonglong * 8)()
+for case in sys.argv[1:]:
+    cfg, n, lanes = (int(x) for x in case.split(':'))
+    wl = W.generate(cfg, n)
+    p = Plan.from_workload(wl, lanes=lanes)
+    pi = torch.from_numpy(wl.pose).to(dev); tg = torch.from_numpy(wl.targets).to(dev); po = torch.empty_like(pi)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    p.solve(pi.data_ptr(), tg.data_ptr(), po.data_ptr(), 0, n, st); torch.cuda.synchronize()
+    L.mbik_debug_prof(buf)
+    p.solve(pi.data_ptr(), tg.data_ptr(), po.data_ptr(), 0, n, st); torch.cuda.synchronize()
+    L.mbik_debug_prof(buf)
+    v = list(buf)
+    inf = p.info()
+    waves = (n + inf['skeletons_per_block'] - 1) // inf['skeletons_per_block']
+    out = dict(cfg=cfg, n=n, lanes=inf['lanes_per_skeleton'], spw=inf['skeletons_per_block'],
+               cycles_per_wave=round(v[7] / waves))
+    out.update({k: round(x / max(1, v[7]), 4) for k, x in zip(NAMES[:7], v[:7])})
+    print(json.dumps(out), flush=True)
+    p.close()

@@ -9,9 +9,10 @@ dev = torch.device('cuda', 0)
 cases = [(2, 4096), (3, 65536), (5, 16384), (4, 32768)]
 if len(sys.argv) > 1:
     cases = [tuple(int(x) for x in c.split(':')) for c in sys.argv[1:]]
-for cfg, n in cases:
+for case in cases:
+    cfg, n = case[0], case[1]
     wl = W.generate(cfg, n)
-    for lanes in [0, 4, 8, 16, 32, 64]:
+    for lanes in (case[2:] or [0, 4, 8, 16, 32, 64]):
         try:
             p = Plan.from_workload(wl, lanes=lanes)
         except Exception as e:
@@ -30,6 +31,7 @@ for cfg, n in cases:
             p.solve(pi.data_ptr(), tg.data_ptr(), po.data_ptr(), 0, n, st)
         e1.record(); torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / reps
+        inf = p.info()
         print(json.dumps(dict(cfg=cfg, n=n, lanes=inf['lanes_per_skeleton'], spw=inf['skeletons_per_block'], ms=round(ms, 3),
                               mskel_s=round(n / ms / 1e3, 3))), flush=True)
         p.close()
