@@ -25,6 +25,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
+VALU_PEAK_TFLOPS = 157.3  # MI355X FP32 vector peak (same guide)
 SKEL_PER_GPU = {2: 4096, 3: 65536, 4: 262144 // 8, 5: 16384}
 METRIC = "skeletons/sec to convergence (32-bone/4-eff, 16 iters) at 1/2/4/8 GPU; bone-quat max-err vs ref"
 
@@ -163,6 +164,7 @@ def main():
     value = total / (wall_max / args.steps)
     alg_bytes = info["algorithmic_bytes_per_skeleton"] * n
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+    alg_flops = info["algorithmic_flops_per_skeleton"] * n
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
@@ -194,6 +196,10 @@ def main():
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "algorithmic_bytes_per_launch": alg_bytes, "kernel_ms": kernel_ms,
                      "note": "latency/VALU-bound serial chain; HBM fraction reported as requested (DESIGN.md §5)"},
+        "valu": {"achieved": alg_flops / (kernel_ms * 1e-3) / 1e12, "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+                 "frac": alg_flops / (kernel_ms * 1e-3) / 1e12 / VALU_PEAK_TFLOPS,
+                 "algorithmic_flops_per_launch": alg_flops,
+                 "note": "SURVEY.md §8(d) flop formula; the bound that applies to this path (DESIGN.md §5)"},
         "gather_ms": gather_ms,
         "parity": parity,
     }

@@ -101,6 +101,7 @@ typedef struct mbik_plan_info {
 	int32_t device;
 	int64_t device_bytes;              /* per-skeleton plan tables resident in HBM */
 	double algorithmic_bytes_per_skeleton; /* pose in/out + targets + plan tables read once */
+	double algorithmic_flops_per_skeleton; /* SURVEY.md §8(d) per-bone-step formula x bone-steps x iterations */
 } mbik_plan_info;
 
 /* Builds the per-topology tables and the per-skeleton setup data for skeletons

@@ -52,7 +52,8 @@ class MbikPlanInfo(C.Structure):
                 ("pin_count", C.c_int32), ("segment_count", C.c_int32), ("level_count", C.c_int32),
                 ("lanes_per_skeleton", C.c_int32), ("skeletons_per_block", C.c_int32),
                 ("max_headings", C.c_int32), ("device", C.c_int32), ("device_bytes", C.c_int64),
-                ("algorithmic_bytes_per_skeleton", C.c_double)]
+                ("algorithmic_bytes_per_skeleton", C.c_double),
+                ("algorithmic_flops_per_skeleton", C.c_double)]
 
 
 class MbikError(RuntimeError):

@@ -589,11 +589,13 @@ void build_schedule(HostPlan &p, int32_t lanes, int64_t nlaunch) {
 	if (lanes > 0) {
 		K = 1 << ceil_log2(lanes);
 	} else {
+		// One lane per segment of the widest sibling level.  The solve is a serial chain
+		// per skeleton (latency-bound), so lanes beyond the sibling parallelism only add
+		// redundant work: measured on MI355X (tools/sweep.py) the widest
+		// level's width is the fastest lane count for C2-C5, also where it leaves the chip
+		// with fewer than one wave per SIMD.
 		K = std::min(64, 1 << ceil_log2(widest));
-		// Fill the chip: >= 4 waves' worth of blocks per CU-quad (1024 single-wave blocks).
-		while (K < 64 && (nlaunch + (64 / K) - 1) / (64 / K) < 1024) K *= 2;
-		// Keep at least ~3 blocks resident per CU (LDS 160 KiB).
-		while (K < 64 && (int64_t)(64 / K) * lds_floats_per_skeleton(p) * 4 > 48 * 1024) K *= 2;
+		(void)nlaunch;
 	}
 	K = std::max(1, std::min(64, K));
 	p.K = K;

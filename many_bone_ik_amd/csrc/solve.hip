@@ -620,7 +620,17 @@ __global__ __launch_bounds__(64) void mbik_solve_kernel(DevPlan t, int first, in
 	float *lds = reinterpret_cast<float *>(lds4) + t.topo_words;
 	const int g = lane >> t.log2K;
 	const int role = lane & (t.K - 1);
-	const int local = blockIdx.x * t.spw + g;
+	// XCD-aware block order: the hardware deals consecutive blocks round-robin to the 8
+	// XCDs (separate L2s), so hand each XCD a contiguous run of skeletons; SoA plan rows
+	// of neighbouring skeletons then share cache lines in one L2 instead of eight.
+	const int nb = gridDim.x, nb8 = nb & ~7, bx = blockIdx.x;
+#ifdef MBIK_ABLATE_XCD
+	const int blk = bx;
+	(void)nb8;
+#else
+	const int blk = bx < nb8 ? (bx & 7) * (nb8 >> 3) + (bx >> 3) : bx;
+#endif
+	const int local = blk * t.spw + g;
 	const bool valid = g < t.spw && local < count;
 	const size_t s = (size_t)first + (size_t)(valid ? local : 0);
 	const int B = t.B, P = t.P, K = t.K;
@@ -693,6 +703,7 @@ struct mbik_plan {
 	DevPlan dev{};
 	int64_t device_bytes = 0;
 	double alg_bytes = 0;
+	double alg_flops = 0;
 	int sched_K = -1;
 	void *d_sched = nullptr; // topology blob (includes the lane schedule)
 	// scratch for mbik_solve_host
@@ -866,9 +877,33 @@ int32_t mbik_plan_create(const mbik_skeleton_desc *desc, const mbik_config *conf
 		for (void *a : p->allocs) (void)hipFree(a);
 		return rc;
 	}
-	// Algorithmic HBM bytes per skeleton (read once + write once).
-	int nlist = (int)h.bone_list.size();
-	p->alg_bytes = (double)h.B * 10 * 4 * 2 + (double)h.P * 12 * 4 + (double)nlist * 9 * 4 +
+	// Algorithmic HBM bytes per skeleton, each byte the solve needs read once and each
+	// output written once: poses in + out, targets, the bone-direction
+	// basis of every bone whose bone-direction frame is read (effector bones and
+	// cone-constrained bones), and the constraint slots.
+	int ndir = 0;
+	for (int b = 0; b < h.B; b++) {
+		bool used = (h.bone_flags[b] & mbik::BF_ORIENT) != 0;
+		for (int e = 0; e < h.P && !used; e++) used = h.eff_bone[e] == b;
+		ndir += used;
+	}
+	// Algorithmic flops: per bone-step 50 H + 14 H [translate] + 72 E_seg
+	// + 465, plus 770 + 140 C - 60 for a constrained bone with C cones; x iterations.
+	double f = 0;
+	for (int sg = 0; sg < h.NS; sg++) {
+		const int H = h.seg_nh[sg], E = h.seg_eff_off[sg + 1] - h.seg_eff_off[sg];
+		const bool tr = (h.seg_flags[sg] & mbik::SF_TRANSLATE) != 0;
+		for (int k = h.seg_bone_off[sg]; k < h.seg_bone_off[sg + 1]; k++) {
+			const int b = h.seg_bones[k];
+			f += 50.0 * H + (tr ? 14.0 * H : 0.0) + 72.0 * E + 465.0;
+			if (h.bone_flags[b] & (mbik::BF_ORIENT | mbik::BF_AXIAL)) {
+				const int C = (h.bone_flags[b] & mbik::BF_ORIENT) ? h.cons_ncones[h.bone_cons[b]] : 0;
+				f += 770.0 + 140.0 * C - 60.0;
+			}
+		}
+	}
+	p->alg_flops = f * h.iterations;
+	p->alg_bytes = (double)h.B * 10 * 4 * 2 + (double)h.P * 12 * 4 + (double)ndir * 9 * 4 +
 			(double)h.NC * (h.cf_stride() * 4.0 + h.cd_stride() * 8.0);
 	h.D.clear(); h.D.shrink_to_fit();
 	h.CF.clear(); h.CF.shrink_to_fit();
@@ -905,6 +940,7 @@ int32_t mbik_plan_get_info(const mbik_plan *p, mbik_plan_info *o) {
 	o->device = p->device;
 	o->device_bytes = p->device_bytes;
 	o->algorithmic_bytes_per_skeleton = p->alg_bytes;
+	o->algorithmic_flops_per_skeleton = p->alg_flops;
 	return MBIK_OK;
 }
 

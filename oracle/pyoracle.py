@@ -13,7 +13,7 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
+LIB_PATH = os.environ.get("ORACLE_LIB") or os.path.join(_HERE, "build", "liboracle.so")  # override: libm study only
 _lib = None
 
 _f32p = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")

@@ -1,0 +1,20 @@
+#!/bin/bash
+# One GPU-box pass for the round's evidence: bench line, kernel-trace stats, PMC traffic.
+#   tools/round_profile.sh <round-tag> [config]
+# Every GPU step has its own time limit; the first failure ends the script.
+set -e
+TAG=${1:-r01}; CFG=${2:-2}
+cd "$(dirname "$0")/.."
+ROOT=$PWD
+OUT=$ROOT/gpurun_out/$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+B="$ROOT/bench.py --config $CFG --steps 20 --warmup 3 --no-cpu-baseline --no-parity"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/ktrace -o run --output-format csv -- python3 $B > $OUT/ktrace.json 2> $OUT/ktrace.log
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o run --output-format csv -- python3 $B > $OUT/fetch.json 2> $OUT/fetch.log
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o run --output-format csv -- python3 $B > $OUT/write.json 2> $OUT/write.log
+N=$(python3 -c "import json,sys; print(json.loads(open('$OUT/ktrace.json').read().strip().splitlines()[-1])['config']['skeletons_per_gpu'])")
+python3 tools/traffic_from_pmc.py $(ls $OUT/fetch/run_counter_collection.csv) $(ls $OUT/write/run_counter_collection.csv) c${CFG}_$N profiles/traffic.json
+cp profiles/traffic.json $OUT/traffic.json
+timeout -k 10 300 python3 bench.py --config $CFG > $OUT/bench.json 2> $OUT/bench.err
+cat $OUT/bench.json
