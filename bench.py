@@ -138,6 +138,18 @@ def main():
         dist.all_reduce(gt, op=dist.ReduceOp.MAX)
         gather_ms = float(gt.item()) * 1e3
 
+    # PCIe-inclusive rate (host buffers in, solve, host buffers out): reported, never `value`
+    pcie = None
+    if rank == 0:
+        plan.solve_host(wl.pose, wl.targets)
+        reps = 5
+        h0 = time.perf_counter()
+        for _ in range(reps):
+            plan.solve_host(wl.pose, wl.targets)
+        hms = (time.perf_counter() - h0) / reps * 1e3
+        pcie = {"ms_per_frame": hms, "skeletons_per_s": n / (hms * 1e-3),
+                "note": "mbik_solve_host: pageable host pose/targets in, solve, poses out"}
+
     # parity spot check of this rank's first skeletons against the oracle (not timed)
     parity = None
     if not args.no_parity and rank == 0:
@@ -201,6 +213,7 @@ def main():
                  "algorithmic_flops_per_launch": alg_flops,
                  "note": "SURVEY.md §8(d) flop formula; the bound that applies to this path (DESIGN.md §5)"},
         "gather_ms": gather_ms,
+        "pcie_inclusive": pcie,
         "parity": parity,
     }
     if world == 1 and not args.no_cpu_baseline:
