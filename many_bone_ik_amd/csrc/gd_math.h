@@ -255,6 +255,7 @@ GDI B3 operator*(const B3 &a, const B3 &b) {
 GDI V3 xform(const B3 &b, V3 v) { return v3(dot(b.r[0], v), dot(b.r[1], v), dot(b.r[2], v)); }
 GDI bool is_finite(const B3 &b) { return is_finite(b.r[0]) && is_finite(b.r[1]) && is_finite(b.r[2]); }
 GDI bool eq(const B3 &a, const B3 &b) { return eq(a.r[0], b.r[0]) && eq(a.r[1], b.r[1]) && eq(a.r[2], b.r[2]); }
+GDI bool eq(const X3 &a, const X3 &b) { return eq(a.b, b.b) && eq(a.o, b.o); }
 GDI V3 get_scale(const B3 &b) {
 	float det = determinant(b);
 	float sg = det == 0 ? 0.0f : (det < 0 ? -1.0f : 1.0f);

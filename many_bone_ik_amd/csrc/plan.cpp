@@ -138,6 +138,7 @@ std::string build_topology(const mbik_skeleton_desc &desc, const mbik_config &cf
 		p.seg_parent[i] = g.parent >= 0 ? new_id[g.parent] : -1;
 		for (int c : g.kept) p.seg_children[i].push_back(new_id[c]);
 		if (g.parent < 0) p.seg_flags[i] |= SF_TRANSLATE;
+		if (g.parent < 0 && cfg.stabilization_passes > 0) p.seg_flags[i] |= SF_STAB;
 		for (int b : g.bones) {
 			p.seg_bones.push_back(b);
 			p.bone_list.push_back(b);
@@ -212,6 +213,10 @@ std::string build_topology(const mbik_skeleton_desc &desc, const mbik_config &cf
 		p.seg_hw.insert(p.seg_hw.end(), w.begin(), w.end());
 		p.seg_nh[i] = h;
 		p.max_headings = std::max(p.max_headings, h);
+		// _get_manual_msd (ik_bone_segment_3d.cpp:114-127): float w_sum += double weight.
+		float ws = 0.0f;
+		for (double x : w) ws = (float)((double)ws + x);
+		p.seg_wsum2.push_back(ws * ws);
 	}
 	// Damping per (segment, bone): _qcp_solver (:227-240); the root segment uses PI (:217-222).
 	p.seg_cos_half_damp.clear();
@@ -557,7 +562,7 @@ std::string build_skeletons(HostPlan &p, int32_t n, const float *setup_pose, con
 // ---------------------------------------------------------------------------------------
 // Launch shape + sibling-level schedule
 // ---------------------------------------------------------------------------------------
-int32_t lds_floats_per_skeleton(const HostPlan &p) { return p.B * 24 + p.P * 25; }
+int32_t lds_floats_per_skeleton(const HostPlan &p) { return p.B * 24 + p.P * 25 + (p.stabilization_passes > 0 ? p.P * 10 : 0); }
 
 // Upper bound of the LDS bytes taken by the topology blob (solve.hip: upload_topology).
 int64_t topology_bytes(const HostPlan &p) {
@@ -567,6 +572,7 @@ int64_t topology_bytes(const HostPlan &p) {
 	ints(p.bone_cons.size()); ints(p.bone_child_eff_off.size()); ints(p.bone_child_effs.size());
 	ints(p.seg_bone_off.size()); ints(p.seg_bones.size()); ints(p.seg_eff_off.size()); ints(p.seg_effs.size());
 	ints(p.seg_eff_hoff.size()); ints(p.seg_nh.size()); ints(p.seg_flags.size()); ints(p.seg_hw_off.size());
+	ints(p.seg_wsum2.size());
 	ints(p.eff_bone.size()); ints(p.eff_path_off.size()); ints(p.eff_path.size()); ints(p.eff_prio.size());
 	ints(p.cons_ncones.size()); ints(2 * p.seg_hw.size()); ints(2 * p.seg_cos_half_damp.size());
 	return (w + 4) * 4;

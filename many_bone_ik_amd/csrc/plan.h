@@ -20,6 +20,8 @@ enum BoneFlags : int32_t {
 
 enum SegFlags : int32_t {
 	SF_TRANSLATE = 1,  // root segment: translate=true, damp=PI (ik_bone_segment_3d.cpp:217-222)
+	SF_STAB = 2,       // root segment built with default_stabilizing_pass_count > 0 (many_bone_ik_3d.cpp:1046;
+	                   // child segments get 0, ik_bone_segment_3d.cpp:398)
 };
 
 // Pose-node parent codes (IKNode3D parent of godot_skeleton_aligned_transform).
@@ -64,6 +66,7 @@ struct HostPlan {
 	std::vector<int32_t> seg_nh, seg_flags, seg_hw_off, seg_height, seg_tin, seg_tout;
 	std::vector<double> seg_hw;                     // heading weights (recursive_create_penalty_array)
 	std::vector<double> seg_cos_half_damp;          // per (segment, bone position): cos(damp / 2.0)
+	std::vector<float> seg_wsum2;                   // _get_manual_msd's (float) w_sum squared, per segment
 	std::vector<int32_t> roots;                     // root segments (segmented_skeletons)
 	std::vector<int32_t> eff_bone, eff_parent_bone, eff_path_off, eff_path;
 	std::vector<float> eff_prio;
@@ -92,7 +95,9 @@ std::string build_skeletons(HostPlan &plan, int32_t n, const float *setup_pose, 
 		int32_t max_cones_in);
 // Chooses lanes-per-skeleton / skeletons-per-block and the sibling-level schedule.
 void build_schedule(HostPlan &plan, int32_t lanes_per_skeleton, int64_t skeletons_in_launch);
-// LDS floats per skeleton used by the kernel.
+// LDS floats per skeleton used by the kernel: L, G (12 per bone), targets + stale cache
+// (12 + 12 per pin), stale flags (1 per pin), and with stabilization the pre-loop target
+// origins (3 per pin) and the manual-MSD terms (7 per pin).
 int32_t lds_floats_per_skeleton(const HostPlan &plan);
 int64_t topology_bytes(const HostPlan &plan);
 

@@ -36,9 +36,11 @@
 using namespace gd;
 
 // Diagnostic cycle accounting (-DMBIK_PROF builds only; tools/prof_phases.py reads it):
-// 0 load, 1 headings+QCP, 2 clamp/slerp/rotate, 3 swing, 4 twist, 5 global pass, 6 store, 7 total.
+// 0 load, 1 headings+QCP, 2 clamp/slerp/rotate, 3 swing, 4 twist, 5 global pass, 6 store, 7 total;
+// sub-phases: 8 step start (P, Lb, Gb), 9 effector_headings (multi-heading segments), 10 QCP
+// adjugate, 11 QCP-to-clamp (step start .. clamp end), 12 slerp round trip.
 #ifdef MBIK_PROF
-__device__ unsigned long long g_mbik_prof[8];
+__device__ unsigned long long g_mbik_prof[16];
 #define MBIK_PROF_PARAM , uint64_t *pf
 #define MBIK_PROF_ARG , pf
 #define MBIK_PROF_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
@@ -60,11 +62,13 @@ namespace {
 	X(int, bone_child_eff_off) X(int, bone_child_effs) X(int, seg_bone_off) X(int, seg_bones)         \
 	X(int, seg_eff_off) X(int, seg_effs) X(int, seg_eff_hoff) X(int, seg_nh) X(int, seg_flags)         \
 	X(int, seg_hw_off) X(int, eff_bone) X(int, eff_path_off) X(int, eff_path) X(float, eff_prio)       \
-	X(int, cons_ncones) X(double, seg_hw) X(double, seg_cos_half_damp) X(int4, sched)
+	X(int, cons_ncones) X(float, seg_wsum2) X(double, seg_hw) X(double, seg_cos_half_damp) X(int4, sched)
 
 struct DevPlan {
 	int B, P, NS, NC, max_cones, nrows, K, log2K, spw, lds_stride;
 	int N, cf_stride, cd_stride;
+	int stab;            // stabilization_passes (root segments only, SF_STAB)
+	int constraint_mode; // ManyBoneIK3D::constraint_mode
 	int topo_words; // blob size in 32-bit words (multiple of 4)
 	const uint4 *topo_blob;
 #define MBIK_DECL(T, name) const T *name; int o_##name;
@@ -232,8 +236,12 @@ struct Headings {
 	double w[7];
 	int mask;
 };
+// oe_mode (stabilization, ik_bone_segment_3d.cpp:135-176): 0 plain; 1 also record the target
+// headings' origin in OE; 2 take that origin from OE (target headings are built once per
+// bone-step, before the retry loop, while tip headings are rebuilt on every pass).
 __device__ __forceinline__ void effector_headings(const DevPlan &t, int e, int b, const X3 &Gb, const float *L,
-		const float *TG, const float *ST, const int *SF, size_t s, const double *hw, Headings &H) {
+		const float *TG, const float *ST, const int *SF, size_t s, const double *hw, Headings &H, float *OE = nullptr,
+		int oe_mode = 0) {
 	X3 E;
 	if (SF[e]) {
 		E = ld_x(ST + 12 * e); // stale bone-direction cache (ik_node_3d.cpp:56-67 never propagates)
@@ -247,7 +255,12 @@ __device__ __forceinline__ void effector_headings(const DevPlan &t, int e, int b
 		E.o = X.o;
 	}
 	const X3 T = ld_x(TG + 12 * e);
-	const V3 oe = E.o;   // target headings: the effector's own bone origin (:97)
+	V3 oe = E.o;         // target headings: the effector's own bone origin (:97)
+	if (oe_mode == 1) {
+		OE[3 * e] = oe.x; OE[3 * e + 1] = oe.y; OE[3 * e + 2] = oe.z;
+	} else if (oe_mode == 2) {
+		oe = v3(OE[3 * e], OE[3 * e + 1], OE[3 * e + 2]);
+	}
 	const V3 ob = Gb.o;  // tip headings: the solved bone's origin (:125)
 	H.ht[0] = T.o - oe;
 	H.hm[0] = E.o - ob;
@@ -374,29 +387,43 @@ __device__ __forceinline__ void swing_twist_y(Q rot, Q &swing, Q &twist) {
 
 // ------------------------------------------------------------------------------------
 // One bone-step: IKBoneSegment3D::_update_optimal_rotation + _set_optimal_rotation
-// (ik_bone_segment_3d.cpp:90-181) with stabilization_passes == 0, constraint_mode false.
+// (ik_bone_segment_3d.cpp:90-181), including the stabilization retry loop (:163-180) of
+// root segments and constraint_mode (:142).  prev_dev is the segment's previous_deviation.
 // ------------------------------------------------------------------------------------
+__device__ __forceinline__ void wave_sync_lds() {
+	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+	__builtin_amdgcn_wave_barrier();
+	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, size_t s, float *L, const float *G, const float *TG,
-		float *ST, int *SF MBIK_PROF_PARAM) {
+		float *ST, int *SF, float *OE, float *MS, double &prev_dev MBIK_PROF_PARAM) {
 	MBIK_PROF_T(pt0);
 	const int b = t.seg_bones[k];
 	const int pp = t.bone_pose_parent[b];
 	const bool hasP = pp != mbik::POSE_PARENT_NONE;
 	const X3 P = pp >= 0 ? ld_x(G + 12 * pp) : xid();
+	const B3 Pinv = inverse(P.b);
+	const bool stab = (t.seg_flags[seg] & mbik::SF_STAB) != 0;
+	const X3 Lprev = ld_x(L + 12 * b); // prev_transform (:136)
+	for (int attempt = 0;; attempt++) {
+	const int oe_mode = stab ? (attempt == 0 ? 1 : 2) : 0;
 	X3 Lb = ld_x(L + 12 * b);
 	const X3 Gb = hasP ? P * Lb : Lb;
 	const bool translate = (t.seg_flags[seg] & mbik::SF_TRANSLATE) != 0;
 	const int e0 = t.seg_eff_off[seg], e1 = t.seg_eff_off[seg + 1];
 	const int nh = t.seg_nh[seg];
+	MBIK_PROF_T(ph0);
+	MBIK_PROF_ADD(8, pt0, ph0);
 	const double *hw = t.seg_hw + t.seg_hw_off[seg];
 
+	if (!t.constraint_mode) {
 	// ---- QCP::weighted_superpose(tip headings, target headings, weights, translate) ----
 	Q qrot;
 	V3 translation = v3(0, 0, 0);
 	Headings H;
 	if (nh == 1) {
 		// one heading in the segment: every lane of the group computes it (qcp.cpp:59-78)
-		effector_headings(t, t.seg_effs[e0], b, Gb, L, TG, ST, SF, s, hw, H);
+		effector_headings(t, t.seg_effs[e0], b, Gb, L, TG, ST, SF, s, hw, H, OE, oe_mode);
 		V3 mvd = H.hm[0], tgt = H.ht[0];
 		if (translate) {
 			double w = H.w[0];
@@ -423,7 +450,8 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, size_t
 				V3 cm[7], ct[7];
 				int mask = 0;
 				if (i < e1) {
-					effector_headings(t, t.seg_effs[i], b, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H);
+					effector_headings(t, t.seg_effs[i], b, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE,
+							oe_mode);
 					mask = H.mask;
 #pragma unroll
 					for (int h = 0; h < 7; h++) {
@@ -457,7 +485,11 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, size_t
 		QSums S = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 		const V3 nmc = mc * -1.0f, ntc = tc * -1.0f;
 		for (int i = e0 + j; i < e1; i += m) {
-			effector_headings(t, t.seg_effs[i], b, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H);
+			MBIK_PROF_T(ph1);
+			effector_headings(t, t.seg_effs[i], b, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE,
+					oe_mode);
+			MBIK_PROF_T(ph2);
+			MBIK_PROF_ADD(9, ph1, ph2);
 #pragma unroll
 			for (int h = 0; h < 7; h++) {
 				if (H.mask & (1 << h)) {
@@ -478,12 +510,19 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, size_t
 					S.zz += (double)(wc1.z * c2.z);
 				}
 			}
+			MBIK_PROF_T(ph5);
+			MBIK_PROF_ADD(14, ph2, ph5);
 		}
+		MBIK_PROF_T(ph6);
 		S.xx = grp_sum(S.xx, m); S.xy = grp_sum(S.xy, m); S.xz = grp_sum(S.xz, m);
 		S.yx = grp_sum(S.yx, m); S.yy = grp_sum(S.yy, m); S.yz = grp_sum(S.yz, m);
 		S.zx = grp_sum(S.zx, m); S.zy = grp_sum(S.zy, m); S.zz = grp_sum(S.zz, m);
 		S.ss1 = grp_sum(S.ss1, m); S.ss2 = grp_sum(S.ss2, m);
+		MBIK_PROF_T(ph3);
+		MBIK_PROF_ADD(15, ph6, ph3);
 		qrot = qcp_adjugate(S);
+		MBIK_PROF_T(ph4);
+		MBIK_PROF_ADD(10, ph3, ph4);
 	}
 
 	MBIK_PROF_T(pt1);
@@ -495,10 +534,13 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, size_t
 #else
 	B3 rot = from_quat(clamp_cos_half(get_rotation_quaternion(from_quat(qrot)), chd));
 #endif
+	MBIK_PROF_T(pc0);
+	MBIK_PROF_ADD(11, pt1, pc0);
 #ifndef MBIK_ABLATE_SLERP
 	rot = slerp_weight0(rot, Gb.b);
 #endif
-	const B3 Pinv = inverse(P.b);
+	MBIK_PROF_T(pc1);
+	MBIK_PROF_ADD(12, pc0, pc1);
 	if (hasP) Lb.b = ((Pinv * rot) * P.b) * Lb.b;
 	X3 Gn = hasP ? P * Lb : Lb;
 	X3 result = {Gn.b, Gn.o + translation};
@@ -509,6 +551,13 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, size_t
 	// Every lane of the group holds identical values, so each writes its own copy (same
 	// bytes) and later reads never depend on another lane's store ordering.
 	for (int c = t.bone_child_eff_off[b]; c < t.bone_child_eff_off[b + 1]; c++) SF[t.bone_child_effs[c]] = 0;
+	} else if (oe_mode == 1) {
+		// constraint_mode still builds the target headings before the loop (:135)
+		Headings H;
+		const double *hw = t.seg_hw + t.seg_hw_off[seg];
+		for (int i = t.seg_eff_off[seg] + j; i < t.seg_eff_off[seg + 1]; i += m)
+			effector_headings(t, t.seg_effs[i], b, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, 1);
+	}
 
 	MBIK_PROF_T(pt2);
 	MBIK_PROF_ADD(2, pt1, pt2);
@@ -574,8 +623,59 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, size_t
 			SF[e] = 1;
 		}
 	}
+	if (!stab) break;
+	{
+		// _get_manual_msd(tip_headings_uniform, target_headings, weights) (:114-127): lanes
+		// build their effectors' terms, every lane of the group sums them in heading order.
+		wave_sync_lds();
+		const X3 Gnow = hasP ? P * Lb : Lb;
+		const double *hw = t.seg_hw + t.seg_hw_off[seg];
+		Headings H;
+		for (int i = t.seg_eff_off[seg] + j; i < t.seg_eff_off[seg + 1]; i += m) {
+			const int e = t.seg_effs[i];
+			effector_headings(t, e, b, Gnow, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, 2);
+#pragma unroll
+			for (int h = 0; h < 7; h++) {
+				if (H.mask & (1 << h)) {
+					const V3 d = H.ht[h] - H.hm[h];
+					MS[7 * e + h] = (float)(H.w[h] * (double)(d.x * d.x + d.y * d.y + d.z * d.z));
+				}
+			}
+		}
+		wave_sync_lds();
+		float msd = 0.0f;
+		for (int i = t.seg_eff_off[seg]; i < t.seg_eff_off[seg + 1]; i++) {
+			const int e = t.seg_effs[i];
+			msd += MS[7 * e];
+#pragma unroll
+			for (int a = 0; a < 3; a++) {
+				if (t.eff_prio[3 * e + a] > 0.0f) {
+					msd += MS[7 * e + 1 + 2 * a];
+					msd += MS[7 * e + 2 + 2 * a];
+				}
+			}
+		}
+		msd /= t.seg_wsum2[seg];
+		if ((double)msd <= prev_dev * 1.0001) {
+			prev_dev = msd;
+			break;
+		}
+		// reject: set_pose(prev_transform) -> IKNode3D::set_transform propagates only when the
+		// local transform changes (ik_node_3d.cpp:69-75), refreshing b's subtree caches.
+		if (!eq(Lb, Lprev)) {
+			st_x(L + 12 * b, Lprev);
+			if (flags & mbik::BF_PINNED) SF[t.bone_pin[b]] = 0;
+			for (int c = t.bone_child_eff_off[b]; c < t.bone_child_eff_off[b + 1]; c++) SF[t.bone_child_effs[c]] = 0;
+		}
+		wave_sync_lds();
+		if (attempt + 1 >= t.stab) break;
+	}
+	} // attempt loop
 	MBIK_PROF_T(pt4);
 	MBIK_PROF_ADD(4, pt3, pt4);
+#ifdef MBIK_PROF
+	if (translate) MBIK_PROF_ADD(13, pt0, pt4);
+#endif
 }
 
 // Iteration-start globals of one segment, root -> tip (IKNode3D::get_global_transform).
@@ -605,7 +705,7 @@ __global__ __launch_bounds__(64) void mbik_solve_kernel(DevPlan t, int first, in
 	extern __shared__ float4 lds4[];
 	const int lane = threadIdx.x;
 #ifdef MBIK_PROF
-	uint64_t pfa[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+	uint64_t pfa[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 	uint64_t *pf = pfa;
 #endif
 	MBIK_PROF_T(pk0);
@@ -639,6 +739,8 @@ __global__ __launch_bounds__(64) void mbik_solve_kernel(DevPlan t, int first, in
 	float *TG = G + 12 * B;
 	float *ST = TG + 12 * P;
 	int *SF = reinterpret_cast<int *>(ST + 12 * P);
+	float *OE = reinterpret_cast<float *>(SF + P); // stabilization only: 3 per pin
+	float *MS = OE + 3 * P;                        // stabilization only: 7 per pin
 	if (valid) {
 		for (int b = role; b < B; b += K)
 			if (t.bone_flags[b] & mbik::BF_IN_LIST) st_x(L + 12 * b, pose_to_xform(pose_in + ((size_t)local * B + b) * 10));
@@ -663,8 +765,9 @@ __global__ __launch_bounds__(64) void mbik_solve_kernel(DevPlan t, int first, in
 		for (int r = 0; r < t.nrows; r++) {
 			const int4 task = t.sched[r * K + role];
 			if (valid && task.x >= seg_lo && task.x <= seg_hi) {
+				double prev_dev = INFINITY; // reset after the segment root bone (:178-180)
 				for (int k = t.seg_bone_off[task.x]; k < t.seg_bone_off[task.x + 1]; k++)
-					bone_step(t, task.x, k, task.y, task.z, s, L, G, TG, ST, SF MBIK_PROF_ARG);
+					bone_step(t, task.x, k, task.y, task.z, s, L, G, TG, ST, SF, OE, MS, prev_dev MBIK_PROF_ARG);
 			}
 			__syncthreads();
 		}
@@ -686,7 +789,7 @@ __global__ __launch_bounds__(64) void mbik_solve_kernel(DevPlan t, int first, in
 	MBIK_PROF_ADD(7, pk0, pk3);
 #ifdef MBIK_PROF
 	if (lane == 0)
-		for (int i = 0; i < 8; i++) atomicAdd(&g_mbik_prof[i], (unsigned long long)pfa[i]);
+		for (int i = 0; i < 16; i++) atomicAdd(&g_mbik_prof[i], (unsigned long long)pfa[i]);
 #endif
 }
 
@@ -846,7 +949,6 @@ int32_t mbik_plan_create(const mbik_skeleton_desc *desc, const mbik_config *conf
 	if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(MBIK_ENODEV, "no HIP device visible");
 	if (device < 0 || device >= ndev) return fail(MBIK_EINVAL, "device index out of range");
 	if (config->constraint_mode) return fail(MBIK_EUNSUPPORTED, "constraint_mode is not implemented on the GPU path yet");
-	if (config->stabilization_passes > 0) return fail(MBIK_EUNSUPPORTED, "stabilization_passes > 0 is not implemented on the GPU path yet");
 	std::unique_ptr<mbik_plan> p(new mbik_plan());
 	p->device = device;
 	std::string err = mbik::build_topology(*desc, *config, p->host);
@@ -863,6 +965,7 @@ int32_t mbik_plan_create(const mbik_skeleton_desc *desc, const mbik_config *conf
 	DevPlan &d = p->dev;
 	d.B = h.B; d.P = h.P; d.NS = h.NS; d.NC = h.NC; d.max_cones = h.max_cones; d.N = h.N;
 	d.cf_stride = h.cf_stride(); d.cd_stride = h.cd_stride();
+	d.stab = h.stabilization_passes; d.constraint_mode = h.constraint_mode;
 	d.lds_stride = (mbik::lds_floats_per_skeleton(h) + 3) & ~3;
 	int rc = 0;
 	rc = rc ? rc : upload(p.get(), h.D, d.D);
@@ -1009,8 +1112,8 @@ int32_t mbik_solve_host(mbik_plan *p, int32_t first, int32_t count, const float 
 
 #ifdef MBIK_PROF
 extern "C" int mbik_debug_prof(unsigned long long *out) {
-	if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mbik_prof), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
-	unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+	if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mbik_prof), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
+	unsigned long long z[16] = {};
 	return hipMemcpyToSymbol(HIP_SYMBOL(g_mbik_prof), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
 #endif

@@ -99,12 +99,13 @@ class Plan:
             self.set_launch(lanes)
 
     @classmethod
-    def from_workload(cls, wl, device=0, lanes=0, iterations=None):
+    def from_workload(cls, wl, device=0, lanes=0, iterations=None, stabilization_passes=0, constraint_mode=False):
         t = wl.topo
         return cls(t.parents, wl.pins(), wl.constraints(), wl.pose, wl.cones, wl.twist,
                    iterations=t.iterations if iterations is None else iterations,
                    default_damp=wl.default_damp, max_cones=wl.cones.shape[2], device=device, lanes=lanes,
-                   bone_damp=wl.bone_damp)
+                   bone_damp=wl.bone_damp, stabilization_passes=stabilization_passes,
+                   constraint_mode=constraint_mode)
 
     def info(self) -> dict:
         inf = MbikPlanInfo()

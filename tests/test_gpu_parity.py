@@ -125,7 +125,7 @@ def test_empty_and_invalid_ranges(mbik):
 def test_unsupported_flags_fail_loudly(mbik):
     wl = W.generate(3, 2)
     t = wl.topo
-    for kw in [dict(constraint_mode=True), dict(stabilization_passes=1)]:
+    for kw in [dict(constraint_mode=True)]:
         with pytest.raises(_lib.MbikError) as e:
             Plan(t.parents, wl.pins(), [], wl.pose, **kw)
         assert e.value.code == _lib.MBIK_EUNSUPPORTED

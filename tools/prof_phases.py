@@ -7,11 +7,12 @@ sys.path.insert(0, '.')
 from many_bone_ik_amd import _lib, workloads as W
 from many_bone_ik_amd.solver import Plan
 
-NAMES = ["load", "headings_qcp", "clamp_slerp_rotate", "swing", "twist", "global_pass", "store", "total"]
+NAMES = ["load", "headings_qcp", "clamp_slerp_rotate", "swing", "twist", "global_pass", "store", "total",
+         "step_start", "eff_headings", "qcp_adjugate", "convert_clamp", "slerp", "translate_steps", "qcp_sums", "grp_sums"]
 dev = torch.device('cuda', 0)
 L = _lib.load()
 L.mbik_debug_prof.argtypes = [C.c_void_p]
-buf = (C.c_ulonglong * 8)()
+buf = (C.c_ulonglong * 16)()
 for case in sys.argv[1:]:
     cfg, n, lanes = (int(x) for x in case.split(':'))
     wl = W.generate(cfg, n)
@@ -27,6 +28,6 @@ for case in sys.argv[1:]:
     waves = (n + inf['skeletons_per_block'] - 1) // inf['skeletons_per_block']
     out = dict(cfg=cfg, n=n, lanes=inf['lanes_per_skeleton'], spw=inf['skeletons_per_block'],
                cycles_per_wave=round(v[7] / waves))
-    out.update({k: round(x / max(1, v[7]), 4) for k, x in zip(NAMES[:7], v[:7])})
+    out.update({k: round(x / max(1, v[7]), 4) for k, x in zip(NAMES, v) if k != "total"})
     print(json.dumps(out), flush=True)
     p.close()
