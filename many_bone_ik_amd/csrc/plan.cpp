@@ -289,6 +289,22 @@ std::string build_topology(const mbik_skeleton_desc &desc, const mbik_config &cf
 	p.seg_height.assign(p.NS, 0);
 	for (int i = 0; i < p.NS; i++)
 		for (int c : p.seg_children[i]) p.seg_height[i] = std::max(p.seg_height[i], p.seg_height[c] + 1);
+	// Staged-heading LDS area (solve.hip, segments solved by several lanes): 12 floats per
+	// heading plus 24 for the exchanged sums.  Segments of one height run concurrently, so
+	// their areas are disjoint; offsets restart at every height.
+	{
+		int maxh = 0;
+		for (int i = 0; i < p.NS; i++) maxh = std::max(maxh, p.seg_height[i]);
+		std::vector<int> used(maxh + 1, 0);
+		p.seg_hbase.assign(p.NS, 0);
+		for (int i = 0; i < p.NS; i++) {
+			if (p.seg_nh[i] < 2) continue;
+			p.seg_hbase[i] = used[p.seg_height[i]];
+			used[p.seg_height[i]] += 12 * p.seg_nh[i] + 24;
+		}
+		p.hs_floats = 0;
+		for (int u : used) p.hs_floats = std::max(p.hs_floats, u);
+	}
 	p.seg_tin.assign(p.NS, 0);
 	p.seg_tout.assign(p.NS, 0);
 	for (int i = 0; i < p.NS; i++) { // post-order: subtree of i = [tin, i]
@@ -562,7 +578,9 @@ std::string build_skeletons(HostPlan &p, int32_t n, const float *setup_pose, con
 // ---------------------------------------------------------------------------------------
 // Launch shape + sibling-level schedule
 // ---------------------------------------------------------------------------------------
-int32_t lds_floats_per_skeleton(const HostPlan &p) { return p.B * 24 + p.P * 25 + (p.stabilization_passes > 0 ? p.P * 10 : 0); }
+int32_t lds_floats_per_skeleton(const HostPlan &p) {
+	return p.B * 24 + p.P * 25 + p.hs_floats + (p.stabilization_passes > 0 ? p.P * 10 : 0);
+}
 
 // Upper bound of the LDS bytes taken by the topology blob (solve.hip: upload_topology).
 int64_t topology_bytes(const HostPlan &p) {
@@ -572,7 +590,7 @@ int64_t topology_bytes(const HostPlan &p) {
 	ints(p.bone_cons.size()); ints(p.bone_child_eff_off.size()); ints(p.bone_child_effs.size());
 	ints(p.seg_bone_off.size()); ints(p.seg_bones.size()); ints(p.seg_eff_off.size()); ints(p.seg_effs.size());
 	ints(p.seg_eff_hoff.size()); ints(p.seg_nh.size()); ints(p.seg_flags.size()); ints(p.seg_hw_off.size());
-	ints(p.seg_wsum2.size());
+	ints(p.seg_wsum2.size()); ints(p.seg_hbase.size());
 	ints(p.eff_bone.size()); ints(p.eff_path_off.size()); ints(p.eff_path.size()); ints(p.eff_prio.size());
 	ints(p.cons_ncones.size()); ints(2 * p.seg_hw.size()); ints(2 * p.seg_cos_half_damp.size());
 	return (w + 4) * 4;

@@ -67,6 +67,8 @@ struct HostPlan {
 	std::vector<double> seg_hw;                     // heading weights (recursive_create_penalty_array)
 	std::vector<double> seg_cos_half_damp;          // per (segment, bone position): cos(damp / 2.0)
 	std::vector<float> seg_wsum2;                   // _get_manual_msd's (float) w_sum squared, per segment
+	std::vector<int32_t> seg_hbase;                 // staged-heading LDS offset (floats) of multi-heading segments
+	int32_t hs_floats = 0;                          // staged-heading LDS floats per skeleton
 	std::vector<int32_t> roots;                     // root segments (segmented_skeletons)
 	std::vector<int32_t> eff_bone, eff_parent_bone, eff_path_off, eff_path;
 	std::vector<float> eff_prio;
@@ -96,7 +98,8 @@ std::string build_skeletons(HostPlan &plan, int32_t n, const float *setup_pose, 
 // Chooses lanes-per-skeleton / skeletons-per-block and the sibling-level schedule.
 void build_schedule(HostPlan &plan, int32_t lanes_per_skeleton, int64_t skeletons_in_launch);
 // LDS floats per skeleton used by the kernel: L, G (12 per bone), targets + stale cache
-// (12 + 12 per pin), stale flags (1 per pin), and with stabilization the pre-loop target
+// (12 + 12 per pin), stale flags (1 per pin), the staged-heading area (hs_floats), and with
+// stabilization the pre-loop target
 // origins (3 per pin) and the manual-MSD terms (7 per pin).
 int32_t lds_floats_per_skeleton(const HostPlan &plan);
 int64_t topology_bytes(const HostPlan &plan);

@@ -44,11 +44,13 @@ __device__ unsigned long long g_mbik_prof[16];
 #define MBIK_PROF_PARAM , uint64_t *pf
 #define MBIK_PROF_ARG , pf
 #define MBIK_PROF_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define MBIK_PROF_SET(v) v = __builtin_amdgcn_s_memtime()
 #define MBIK_PROF_ADD(i, a, b) pf[i] += (b) - (a)
 #else
 #define MBIK_PROF_PARAM
 #define MBIK_PROF_ARG
 #define MBIK_PROF_T(v)
+#define MBIK_PROF_SET(v)
 #define MBIK_PROF_ADD(i, a, b)
 #endif
 
@@ -62,12 +64,13 @@ namespace {
 	X(int, bone_child_eff_off) X(int, bone_child_effs) X(int, seg_bone_off) X(int, seg_bones)         \
 	X(int, seg_eff_off) X(int, seg_effs) X(int, seg_eff_hoff) X(int, seg_nh) X(int, seg_flags)         \
 	X(int, seg_hw_off) X(int, eff_bone) X(int, eff_path_off) X(int, eff_path) X(float, eff_prio)       \
-	X(int, cons_ncones) X(float, seg_wsum2) X(double, seg_hw) X(double, seg_cos_half_damp) X(int4, sched)
+	X(int, cons_ncones) X(float, seg_wsum2) X(int, seg_hbase) X(double, seg_hw) X(double, seg_cos_half_damp) X(int4, sched)
 
 struct DevPlan {
 	int B, P, NS, NC, max_cones, nrows, K, log2K, spw, lds_stride;
 	int N, cf_stride, cd_stride;
 	int stab;            // stabilization_passes (root segments only, SF_STAB)
+	int hs_floats;       // staged-heading LDS floats per skeleton
 	int constraint_mode; // ManyBoneIK3D::constraint_mode
 	int topo_words; // blob size in 32-bit words (multiple of 4)
 	const uint4 *topo_blob;
@@ -112,15 +115,6 @@ __device__ __forceinline__ B3 ld_soa_basis(const float *a, int item, int fields,
 				soa(a, item, fields, f0 + 3 * i + 2, N, s));
 	return b;
 }
-__device__ __forceinline__ double grp_sum(double v, int m) {
-	for (int o = 1; o < m; o <<= 1) v += __shfl_xor(v, o, 64);
-	return v;
-}
-__device__ __forceinline__ float grp_sum(float v, int m) {
-	for (int o = 1; o < m; o <<= 1) v += __shfl_xor(v, o, 64);
-	return v;
-}
-__device__ __forceinline__ V3 grp_sum(V3 v, int m) { return v3(grp_sum(v.x, m), grp_sum(v.y, m), grp_sum(v.z, m)); }
 
 // IKBoneSegment3D::clamp_to_cos_half_angle (ik_bone_segment_3d.cpp:97-112)
 __device__ __forceinline__ Q clamp_cos_half(Q q, double c) {
@@ -395,15 +389,32 @@ __device__ __forceinline__ void wave_sync_lds() {
 	__builtin_amdgcn_wave_barrier();
 	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+// Staged-heading record (multi-lane segments): the 11 QCP::inner_product terms of one heading
+// pair, as floats -- wc1_a * c2_b (a, b = x, y, z), dot(wc1, c1), dot(c2, c2).
+constexpr int HS_REC = 12;
+__device__ __forceinline__ void qcp_terms(const V3 wc1, const V3 c1, const V3 c2, float *r) {
+	r[0] = wc1.x * c2.x; r[1] = wc1.x * c2.y; r[2] = wc1.x * c2.z;
+	r[3] = wc1.y * c2.x; r[4] = wc1.y * c2.y; r[5] = wc1.y * c2.z;
+	r[6] = wc1.z * c2.x; r[7] = wc1.z * c2.y; r[8] = wc1.z * c2.z;
+	r[9] = dot(wc1, c1);
+	r[10] = dot(c2, c2);
+}
+// STAB: the plan has stabilization passes (a separate instantiation keeps the retry loop and
+// its LDS staging out of the default kernel).
+template <bool STAB>
 __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, size_t s, float *L, const float *G, const float *TG,
-		float *ST, int *SF, float *OE, float *MS, double &prev_dev MBIK_PROF_PARAM) {
+		float *ST, int *SF, float *HS, float *OE, float *MS, double &prev_dev MBIK_PROF_PARAM) {
 	MBIK_PROF_T(pt0);
+#ifdef MBIK_PROF
+	uint64_t pt1 = pt0, pt3 = pt0;
+	const bool seg_translate = (t.seg_flags[seg] & mbik::SF_TRANSLATE) != 0;
+#endif
 	const int b = t.seg_bones[k];
 	const int pp = t.bone_pose_parent[b];
 	const bool hasP = pp != mbik::POSE_PARENT_NONE;
 	const X3 P = pp >= 0 ? ld_x(G + 12 * pp) : xid();
 	const B3 Pinv = inverse(P.b);
-	const bool stab = (t.seg_flags[seg] & mbik::SF_STAB) != 0;
+	const bool stab = STAB && (t.seg_flags[seg] & mbik::SF_STAB) != 0;
 	const X3 Lprev = ld_x(L + 12 * b); // prev_transform (:136)
 	for (int attempt = 0;; attempt++) {
 	const int oe_mode = stab ? (attempt == 0 ? 1 : 2) : 0;
@@ -416,7 +427,7 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, size_t
 	MBIK_PROF_ADD(8, pt0, ph0);
 	const double *hw = t.seg_hw + t.seg_hw_off[seg];
 
-	if (!t.constraint_mode) {
+	if (!(STAB && t.constraint_mode)) { // constraint_mode is refused at plan creation
 	// ---- QCP::weighted_superpose(tip headings, target headings, weights, translate) ----
 	Q qrot;
 	V3 translation = v3(0, 0, 0);
@@ -437,57 +448,36 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, size_t
 			translation = tc - mc;
 		}
 		qrot = qcp_single(mvd, tgt);
-	} else {
+	} else if (m == 1) {
+		// Several headings, one lane: QCP::move_to_weighted_center (qcp.cpp:139-160, float)
+		// and QCP::inner_product (:162-218, fp64) straight from registers, heading by heading
+		// in the reference's order.  The translate case builds the headings twice, as the
+		// reference's weighted_superpose does.
 		V3 mc = v3(0, 0, 0), tc = v3(0, 0, 0);
 		if (translate) {
-			// QCP::move_to_weighted_center (qcp.cpp:139-160) accumulates in float, heading by
-			// heading.  Lanes build their effectors' headings in parallel, then every lane adds
-			// the broadcast contributions in the reference's order (effector list order).
 			double wsum = 0;
-			const int base = (threadIdx.x & 63) & ~(m - 1);
-			for (int r0 = e0; r0 < e1; r0 += m) {
-				const int i = r0 + j;
-				V3 cm[7], ct[7];
-				int mask = 0;
-				if (i < e1) {
-					effector_headings(t, t.seg_effs[i], b, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE,
-							oe_mode);
-					mask = H.mask;
+			for (int i = e0; i < e1; i++) {
+				effector_headings(t, t.seg_effs[i], b, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, oe_mode);
 #pragma unroll
-					for (int h = 0; h < 7; h++) {
-						cm[h] = H.hm[h] * (float)H.w[h];
-						ct[h] = H.ht[h] * (float)H.w[h];
-						if (mask & (1 << h)) wsum += H.w[h];
-					}
-				}
-				const int cnt = min(m, e1 - r0);
-				for (int jj = 0; jj < cnt; jj++) {
-					const int mj = __shfl(mask, base + jj, 64);
-#pragma unroll
-					for (int h = 0; h < 7; h++) {
-						V3 a = v3(__shfl(cm[h].x, base + jj, 64), __shfl(cm[h].y, base + jj, 64), __shfl(cm[h].z, base + jj, 64));
-						V3 c = v3(__shfl(ct[h].x, base + jj, 64), __shfl(ct[h].y, base + jj, 64), __shfl(ct[h].z, base + jj, 64));
-						if (mj & (1 << h)) {
-							mc = mc + a;
-							tc = tc + c;
-						}
+				for (int h = 0; h < 7; h++) {
+					if (H.mask & (1 << h)) {
+						mc = mc + H.hm[h] * (float)H.w[h];
+						tc = tc + H.ht[h] * (float)H.w[h];
+						wsum += H.w[h];
 					}
 				}
 			}
-			wsum = grp_sum(wsum, m);
 			if (wsum > 0) {
 				mc = divs(mc, (float)wsum);
 				tc = divs(tc, (float)wsum);
 			}
 			translation = tc - mc;
 		}
-		// QCP::inner_product(target, moved) (qcp.cpp:162-218)
 		QSums S = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 		const V3 nmc = mc * -1.0f, ntc = tc * -1.0f;
-		for (int i = e0 + j; i < e1; i += m) {
+		for (int i = e0; i < e1; i++) {
 			MBIK_PROF_T(ph1);
-			effector_headings(t, t.seg_effs[i], b, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE,
-					oe_mode);
+			effector_headings(t, t.seg_effs[i], b, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, oe_mode);
 			MBIK_PROF_T(ph2);
 			MBIK_PROF_ADD(9, ph1, ph2);
 #pragma unroll
@@ -510,22 +500,148 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, size_t
 					S.zz += (double)(wc1.z * c2.z);
 				}
 			}
-			MBIK_PROF_T(ph5);
-			MBIK_PROF_ADD(14, ph2, ph5);
+			MBIK_PROF_T(ph6);
+			MBIK_PROF_ADD(14, ph2, ph6);
 		}
-		MBIK_PROF_T(ph6);
-		S.xx = grp_sum(S.xx, m); S.xy = grp_sum(S.xy, m); S.xz = grp_sum(S.xz, m);
-		S.yx = grp_sum(S.yx, m); S.yy = grp_sum(S.yy, m); S.yz = grp_sum(S.yz, m);
-		S.zx = grp_sum(S.zx, m); S.zy = grp_sum(S.zy, m); S.zz = grp_sum(S.zz, m);
-		S.ss1 = grp_sum(S.ss1, m); S.ss2 = grp_sum(S.ss2, m);
+		MBIK_PROF_T(ph7);
+		qrot = qcp_adjugate(S);
+		MBIK_PROF_T(ph8);
+		MBIK_PROF_ADD(10, ph7, ph8);
+	} else {
+		// Several headings, several lanes.  Every sum of QCP::move_to_weighted_center
+		// (qcp.cpp:139-160, float) and QCP::inner_product (:162-218, fp64) is one accumulator
+		// over the headings in the reference's order (effector-list order; origin, +axis,
+		// -axis per prioritised axis), and the accumulators are independent of each other:
+		//   1. lanes build their effectors' headings into the segment's LDS area, one
+		//      12-float record per heading: the inner-product terms (9 products wc1_a*c2_b,
+		//      dot(wc1,c1), dot(c2,c2)), or for translate the raw target/tip headings;
+		//   2. translate only: lane j takes the centroid sums q = j, j+m, ... < 7; the results
+		//      go through LDS and the lanes turn their records into centred terms;
+		//   3. lane j takes the inner-product sums q = j, j+m, ... < 11, exchanged through LDS.
+		// Each sum is accumulated in exactly the reference's order and rounding.
+		float *hsg = HS + t.seg_hbase[seg];
+		double *ex = reinterpret_cast<double *>(hsg + HS_REC * nh);
+		for (int i = e0 + j; i < e1; i += m) {
+			MBIK_PROF_T(ph1);
+			effector_headings(t, t.seg_effs[i], b, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, oe_mode);
+			MBIK_PROF_T(ph2);
+			MBIK_PROF_ADD(9, ph1, ph2);
+			float *r = hsg + HS_REC * t.seg_eff_hoff[i];
+#pragma unroll
+			for (int h = 0; h < 7; h++) {
+				if (H.mask & (1 << h)) {
+					if (translate) {
+						r[0] = H.ht[h].x; r[1] = H.ht[h].y; r[2] = H.ht[h].z;
+						r[3] = H.hm[h].x; r[4] = H.hm[h].y; r[5] = H.hm[h].z;
+					} else {
+						qcp_terms(H.ht[h] * (float)H.w[h], H.ht[h], H.hm[h], r);
+					}
+					r += HS_REC;
+				}
+			}
+		}
+		wave_sync_lds();
+		MBIK_PROF_T(ph5);
+		if (translate) {
+			// centroid sums: q 0-2 moved centre (tip headings), 3-5 target centre, 6 weight sum
+			float fa0 = 0.0f, fa1 = 0.0f;
+			double wacc = 0.0;
+			const int q0 = j, q1 = j + m;
+			const int o0 = q0 < 3 ? 3 + q0 : q0 - 3, o1 = q1 < 3 ? 3 + q1 : q1 - 3;
+			for (int c = 0; c < nh; c++) {
+				const float *r = hsg + HS_REC * c;
+				const double w = hw[c];
+				const float wf = (float)w;
+				if (q0 < 6) fa0 = fa0 + r[o0] * wf;
+				if (q1 < 6) fa1 = fa1 + r[o1] * wf;
+				wacc += w;
+			}
+			if (q0 < 6) ex[q0] = (double)fa0;
+			if (q1 < 6) ex[q1] = (double)fa1;
+			if (j == 0) ex[6] = wacc;
+			if (m == 2) { // q = j + 4 (target centre y, z) as well
+				float fa2 = 0.0f;
+				for (int c = 0; c < nh; c++) fa2 = fa2 + hsg[HS_REC * c + j + 1] * (float)hw[c];
+				ex[j + 4] = (double)fa2;
+			}
+			wave_sync_lds();
+			V3 mc = v3((float)ex[0], (float)ex[1], (float)ex[2]);
+			V3 tc = v3((float)ex[3], (float)ex[4], (float)ex[5]);
+			const double wsum = ex[6];
+			if (wsum > 0) {
+				mc = divs(mc, (float)wsum);
+				tc = divs(tc, (float)wsum);
+			}
+			translation = tc - mc;
+			const V3 nmc = mc * -1.0f, ntc = tc * -1.0f;
+			wave_sync_lds();
+			for (int c = j; c < nh; c += m) {
+				float *r = hsg + HS_REC * c;
+				const V3 c1 = v3(r[0], r[1], r[2]) + ntc;
+				const V3 c2 = v3(r[3], r[4], r[5]) + nmc;
+				qcp_terms(c1 * (float)hw[c], c1, c2, r);
+			}
+			wave_sync_lds();
+		}
+		// inner-product sums q = j + u*m < 11: q < 10 -> (double)term, q == 10 -> w * (double)term
+		{
+			double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+			const int q0 = j, q1 = j + m, q2 = j + 2 * m;
+			int c = 0;
+			for (; c + 2 <= nh; c += 2) {
+				const float *r = hsg + HS_REC * c;
+				const double w0 = hw[c], w1 = hw[c + 1];
+				const float x0 = r[q0], x1 = r[q1 < 11 ? q1 : 0], x2 = r[q2 < 11 ? q2 : 0];
+				const float y0 = r[HS_REC + q0], y1 = r[HS_REC + (q1 < 11 ? q1 : 0)], y2 = r[HS_REC + (q2 < 11 ? q2 : 0)];
+				a0 += q0 == 10 ? w0 * (double)x0 : (double)x0;
+				a1 += q1 == 10 ? w0 * (double)x1 : (double)x1;
+				a2 += q2 == 10 ? w0 * (double)x2 : (double)x2;
+				a0 += q0 == 10 ? w1 * (double)y0 : (double)y0;
+				a1 += q1 == 10 ? w1 * (double)y1 : (double)y1;
+				a2 += q2 == 10 ? w1 * (double)y2 : (double)y2;
+			}
+			for (; c < nh; c++) {
+				const float *r = hsg + HS_REC * c;
+				const double w0 = hw[c];
+				const float x0 = r[q0], x1 = r[q1 < 11 ? q1 : 0], x2 = r[q2 < 11 ? q2 : 0];
+				a0 += q0 == 10 ? w0 * (double)x0 : (double)x0;
+				a1 += q1 == 10 ? w0 * (double)x1 : (double)x1;
+				a2 += q2 == 10 ? w0 * (double)x2 : (double)x2;
+			}
+			if (q0 < 11) ex[q0] = a0;
+			if (q1 < 11) ex[q1] = a1;
+			if (q2 < 11) ex[q2] = a2;
+			if (m == 2) {
+				// q = j + 6, j + 8, j + 10 as well
+				double b0 = 0.0, b1 = 0.0, b2 = 0.0;
+				const int p0 = j + 6, p1 = j + 8, p2 = j + 10;
+				for (c = 0; c < nh; c++) {
+					const float *r = hsg + HS_REC * c;
+					const double w0 = hw[c];
+					b0 += (double)r[p0];
+					b1 += (double)r[p1];
+					if (p2 < 11) b2 += w0 * (double)r[p2];
+				}
+				ex[p0] = b0;
+				ex[p1] = b1;
+				if (p2 < 11) ex[p2] = b2;
+			}
+		}
+		wave_sync_lds();
+		QSums S;
+		S.xx = ex[0]; S.xy = ex[1]; S.xz = ex[2];
+		S.yx = ex[3]; S.yy = ex[4]; S.yz = ex[5];
+		S.zx = ex[6]; S.zy = ex[7]; S.zz = ex[8];
+		S.ss1 = ex[9]; S.ss2 = ex[10];
+		wave_sync_lds();
 		MBIK_PROF_T(ph3);
-		MBIK_PROF_ADD(15, ph6, ph3);
+		MBIK_PROF_ADD(14, ph5, ph3);
 		qrot = qcp_adjugate(S);
 		MBIK_PROF_T(ph4);
 		MBIK_PROF_ADD(10, ph3, ph4);
 	}
 
-	MBIK_PROF_T(pt1);
+	MBIK_PROF_SET(pt1);
 	MBIK_PROF_ADD(1, pt0, pt1);
 	// ---- damp clamp, slerp(…, 0), rotate, translate, set_global_pose (:144-154) ----
 	const double chd = t.seg_cos_half_damp[k];
@@ -551,7 +667,7 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, size_t
 	// Every lane of the group holds identical values, so each writes its own copy (same
 	// bytes) and later reads never depend on another lane's store ordering.
 	for (int c = t.bone_child_eff_off[b]; c < t.bone_child_eff_off[b + 1]; c++) SF[t.bone_child_effs[c]] = 0;
-	} else if (oe_mode == 1) {
+	} else if (STAB && oe_mode == 1) {
 		// constraint_mode still builds the target headings before the loop (:135)
 		Headings H;
 		const double *hw = t.seg_hw + t.seg_hw_off[seg];
@@ -586,7 +702,7 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, size_t
 			swung = true;
 		}
 	}
-	MBIK_PROF_T(pt3);
+	MBIK_PROF_SET(pt3);
 	MBIK_PROF_ADD(3, pt2, pt3);
 	// ---- Kusudama: twist snap (ik_kusudama_3d.cpp:117-132) ----
 	bool twist_changed = false;
@@ -674,7 +790,7 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, size_t
 	MBIK_PROF_T(pt4);
 	MBIK_PROF_ADD(4, pt3, pt4);
 #ifdef MBIK_PROF
-	if (translate) MBIK_PROF_ADD(13, pt0, pt4);
+	if (seg_translate) MBIK_PROF_ADD(13, pt0, pt4);
 #endif
 }
 
@@ -700,6 +816,7 @@ __device__ void write_pose(const X3 &t, float *out) {
 	out[7] = sc.x; out[8] = sc.y; out[9] = sc.z;
 }
 
+template <bool STAB>
 __global__ __launch_bounds__(64) void mbik_solve_kernel(DevPlan t, int first, int count, const float *__restrict__ pose_in,
 		const float *__restrict__ targets, float *__restrict__ pose_out, int iterations, int seg_lo, int seg_hi) {
 	extern __shared__ float4 lds4[];
@@ -738,8 +855,9 @@ __global__ __launch_bounds__(64) void mbik_solve_kernel(DevPlan t, int first, in
 	float *G = L + 12 * B;
 	float *TG = G + 12 * B;
 	float *ST = TG + 12 * P;
-	int *SF = reinterpret_cast<int *>(ST + 12 * P);
-	float *OE = reinterpret_cast<float *>(SF + P); // stabilization only: 3 per pin
+	float *HS = ST + 12 * P;                        // staged headings (t.seg_hbase), 16-B aligned
+	int *SF = reinterpret_cast<int *>(HS + t.hs_floats);
+	float *OE = reinterpret_cast<float *>(SF + P);  // stabilization only: 3 per pin
 	float *MS = OE + 3 * P;                        // stabilization only: 7 per pin
 	if (valid) {
 		for (int b = role; b < B; b += K)
@@ -767,7 +885,7 @@ __global__ __launch_bounds__(64) void mbik_solve_kernel(DevPlan t, int first, in
 			if (valid && task.x >= seg_lo && task.x <= seg_hi) {
 				double prev_dev = INFINITY; // reset after the segment root bone (:178-180)
 				for (int k = t.seg_bone_off[task.x]; k < t.seg_bone_off[task.x + 1]; k++)
-					bone_step(t, task.x, k, task.y, task.z, s, L, G, TG, ST, SF, OE, MS, prev_dev MBIK_PROF_ARG);
+					bone_step<STAB>(t, task.x, k, task.y, task.z, s, L, G, TG, ST, SF, HS, OE, MS, prev_dev MBIK_PROF_ARG);
 			}
 			__syncthreads();
 		}
@@ -909,9 +1027,13 @@ int launch(mbik_plan *p, int first, int count, const float *pose_in, const float
 	size_t lds = ((size_t)h.spw * p->dev.lds_stride + p->dev.topo_words) * sizeof(float);
 	if (lds > 160 * 1024) return fail(MBIK_EUNSUPPORTED, "skeleton too large for LDS at this lane count");
 	static std::once_flag once;
-	std::call_once(once, [] { (void)hipFuncSetAttribute((const void *)mbik_solve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); });
+	std::call_once(once, [] {
+		(void)hipFuncSetAttribute((const void *)mbik_solve_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+		(void)hipFuncSetAttribute((const void *)mbik_solve_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+	});
 	unsigned blocks = (unsigned)((count + h.spw - 1) / h.spw);
-	hipLaunchKernelGGL(mbik_solve_kernel, dim3(blocks), dim3(64), lds, stream, p->dev, first, count, pose_in, targets, pose_out,
+	auto kern = h.stabilization_passes > 0 ? mbik_solve_kernel<true> : mbik_solve_kernel<false>;
+	hipLaunchKernelGGL(kern, dim3(blocks), dim3(64), lds, stream, p->dev, first, count, pose_in, targets, pose_out,
 			iterations, seg_lo, seg_hi);
 	hipError_t e = hipGetLastError();
 	if (e != hipSuccess) return fail(MBIK_EHIP, std::string("kernel launch failed: ") + hipGetErrorString(e));
@@ -965,7 +1087,7 @@ int32_t mbik_plan_create(const mbik_skeleton_desc *desc, const mbik_config *conf
 	DevPlan &d = p->dev;
 	d.B = h.B; d.P = h.P; d.NS = h.NS; d.NC = h.NC; d.max_cones = h.max_cones; d.N = h.N;
 	d.cf_stride = h.cf_stride(); d.cd_stride = h.cd_stride();
-	d.stab = h.stabilization_passes; d.constraint_mode = h.constraint_mode;
+	d.stab = h.stabilization_passes; d.constraint_mode = h.constraint_mode; d.hs_floats = h.hs_floats;
 	d.lds_stride = (mbik::lds_floats_per_skeleton(h) + 3) & ~3;
 	int rc = 0;
 	rc = rc ? rc : upload(p.get(), h.D, d.D);

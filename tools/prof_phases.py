@@ -8,7 +8,7 @@ from many_bone_ik_amd import _lib, workloads as W
 from many_bone_ik_amd.solver import Plan
 
 NAMES = ["load", "headings_qcp", "clamp_slerp_rotate", "swing", "twist", "global_pass", "store", "total",
-         "step_start", "eff_headings", "qcp_adjugate", "convert_clamp", "slerp", "translate_steps", "qcp_sums", "grp_sums"]
+         "step_start", "eff_headings", "qcp_adjugate", "convert_clamp", "slerp", "translate_steps", "qcp_centroid_sums"]
 dev = torch.device('cuda', 0)
 L = _lib.load()
 L.mbik_debug_prof.argtypes = [C.c_void_p]
