@@ -40,7 +40,7 @@ using namespace gd;
 // sub-phases: 8 step start (P, Lb, Gb), 9 effector_headings (multi-heading segments), 10 QCP
 // adjugate, 11 QCP-to-clamp (step start .. clamp end), 12 slerp round trip.
 #ifdef MBIK_PROF
-__device__ unsigned long long g_mbik_prof[16];
+__device__ unsigned long long g_mbik_prof[24];
 #define MBIK_PROF_PARAM , uint64_t *pf
 #define MBIK_PROF_ARG , pf
 #define MBIK_PROF_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
@@ -243,7 +243,17 @@ __device__ __forceinline__ void effector_headings(const DevPlan &t, int e, int b
 		X3 X = Gb;
 		const int off = t.eff_path_off[e];
 		const int de = t.eff_path_off[e + 1] - off - 1;
-		for (int d = t.bone_depth[b] + 1; d <= de; d++) X = X * ld_x(L + 12 * t.eff_path[off + d]);
+		int d = t.bone_depth[b] + 1;
+		if (d <= de) {
+			// software-pipelined: the next path bone's local pose loads during this product
+			X3 Ln = ld_x(L + 12 * t.eff_path[off + d]);
+			for (; d < de; d++) {
+				const X3 Lc = Ln;
+				Ln = ld_x(L + 12 * t.eff_path[off + d + 1]);
+				X = X * Lc;
+			}
+			X = X * Ln;
+		}
 		const int eb = t.eff_bone[e];
 		E.b = X.b * ld_soa_basis(t.D, eb, 9, 0, t.N, s);
 		E.o = X.o;
@@ -548,12 +558,32 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, size_t
 			double wacc = 0.0;
 			const int q0 = j, q1 = j + m;
 			const int o0 = q0 < 3 ? 3 + q0 : q0 - 3, o1 = q1 < 3 ? 3 + q1 : q1 - 3;
-			for (int c = 0; c < nh; c++) {
+			const int p0 = q0 < 6 ? o0 : 0, p1 = q1 < 6 ? o1 : 0;
+			int c = 0;
+			for (; c + 4 <= nh; c += 4) { // 4 headings per LDS round trip
+				const float *r = hsg + HS_REC * c;
+				float x0[4], x1[4];
+				double w[4];
+#pragma unroll
+				for (int u = 0; u < 4; u++) {
+					x0[u] = r[HS_REC * u + p0];
+					x1[u] = r[HS_REC * u + p1];
+					w[u] = hw[c + u];
+				}
+#pragma unroll
+				for (int u = 0; u < 4; u++) {
+					const float wf = (float)w[u];
+					fa0 = fa0 + x0[u] * wf;
+					fa1 = fa1 + x1[u] * wf;
+					wacc += w[u];
+				}
+			}
+			for (; c < nh; c++) {
 				const float *r = hsg + HS_REC * c;
 				const double w = hw[c];
 				const float wf = (float)w;
-				if (q0 < 6) fa0 = fa0 + r[o0] * wf;
-				if (q1 < 6) fa1 = fa1 + r[o1] * wf;
+				fa0 = fa0 + r[p0] * wf;
+				fa1 = fa1 + r[p1] * wf;
 				wacc += w;
 			}
 			if (q0 < 6) ex[q0] = (double)fa0;
@@ -587,18 +617,25 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, size_t
 		{
 			double a0 = 0.0, a1 = 0.0, a2 = 0.0;
 			const int q0 = j, q1 = j + m, q2 = j + 2 * m;
+			const int i0 = q0 < 11 ? q0 : 0, i1 = q1 < 11 ? q1 : 0, i2 = q2 < 11 ? q2 : 0;
 			int c = 0;
-			for (; c + 2 <= nh; c += 2) {
+			for (; c + 4 <= nh; c += 4) { // 4 headings per LDS round trip
 				const float *r = hsg + HS_REC * c;
-				const double w0 = hw[c], w1 = hw[c + 1];
-				const float x0 = r[q0], x1 = r[q1 < 11 ? q1 : 0], x2 = r[q2 < 11 ? q2 : 0];
-				const float y0 = r[HS_REC + q0], y1 = r[HS_REC + (q1 < 11 ? q1 : 0)], y2 = r[HS_REC + (q2 < 11 ? q2 : 0)];
-				a0 += q0 == 10 ? w0 * (double)x0 : (double)x0;
-				a1 += q1 == 10 ? w0 * (double)x1 : (double)x1;
-				a2 += q2 == 10 ? w0 * (double)x2 : (double)x2;
-				a0 += q0 == 10 ? w1 * (double)y0 : (double)y0;
-				a1 += q1 == 10 ? w1 * (double)y1 : (double)y1;
-				a2 += q2 == 10 ? w1 * (double)y2 : (double)y2;
+				float x0[4], x1[4], x2[4];
+				double w[4];
+#pragma unroll
+				for (int u = 0; u < 4; u++) {
+					x0[u] = r[HS_REC * u + i0];
+					x1[u] = r[HS_REC * u + i1];
+					x2[u] = r[HS_REC * u + i2];
+					w[u] = hw[c + u];
+				}
+#pragma unroll
+				for (int u = 0; u < 4; u++) {
+					a0 += q0 == 10 ? w[u] * (double)x0[u] : (double)x0[u];
+					a1 += q1 == 10 ? w[u] * (double)x1[u] : (double)x1[u];
+					a2 += q2 == 10 ? w[u] * (double)x2[u] : (double)x2[u];
+				}
 			}
 			for (; c < nh; c++) {
 				const float *r = hsg + HS_REC * c;
@@ -636,6 +673,12 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, size_t
 		wave_sync_lds();
 		MBIK_PROF_T(ph3);
 		MBIK_PROF_ADD(14, ph5, ph3);
+#ifdef MBIK_PROF
+		if (translate) {
+			MBIK_PROF_ADD(15, ph0, ph5);
+			MBIK_PROF_ADD(16, ph5, ph3);
+		}
+#endif
 		qrot = qcp_adjugate(S);
 		MBIK_PROF_T(ph4);
 		MBIK_PROF_ADD(10, ph3, ph4);
@@ -677,6 +720,9 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, size_t
 
 	MBIK_PROF_T(pt2);
 	MBIK_PROF_ADD(2, pt1, pt2);
+#ifdef MBIK_PROF
+	if (seg_translate) MBIK_PROF_ADD(17, pt1, pt2);
+#endif
 	// ---- Kusudama: orientation (swing) snap (ik_kusudama_3d.cpp:347-376) ----
 	const int flags = t.bone_flags[b];
 	bool swung = false;
@@ -796,12 +842,16 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, size_t
 
 // Iteration-start globals of one segment, root -> tip (IKNode3D::get_global_transform).
 __device__ void global_pass(const DevPlan &t, int seg, const float *L, float *G) {
+	X3 Gprev = xid();
 	for (int k = t.seg_bone_off[seg + 1] - 1; k >= t.seg_bone_off[seg]; k--) {
 		const int b = t.seg_bones[k];
 		const int pp = t.bone_pose_parent[b];
 		X3 Lb = ld_x(L + 12 * b);
-		X3 Gb = pp >= 0 ? ld_x(G + 12 * pp) * Lb : (pp == mbik::POSE_PARENT_ORIGIN ? xid() * Lb : Lb);
+		X3 Gb;
+		if (k < t.seg_bone_off[seg + 1] - 1) Gb = Gprev * Lb; // parent = the bone just done
+		else Gb = pp >= 0 ? ld_x(G + 12 * pp) * Lb : (pp == mbik::POSE_PARENT_ORIGIN ? xid() * Lb : Lb);
 		st_x(G + 12 * b, Gb);
+		Gprev = Gb;
 	}
 }
 
@@ -822,7 +872,7 @@ __global__ __launch_bounds__(64) void mbik_solve_kernel(DevPlan t, int first, in
 	extern __shared__ float4 lds4[];
 	const int lane = threadIdx.x;
 #ifdef MBIK_PROF
-	uint64_t pfa[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+	uint64_t pfa[24] = {};
 	uint64_t *pf = pfa;
 #endif
 	MBIK_PROF_T(pk0);
@@ -907,7 +957,7 @@ __global__ __launch_bounds__(64) void mbik_solve_kernel(DevPlan t, int first, in
 	MBIK_PROF_ADD(7, pk0, pk3);
 #ifdef MBIK_PROF
 	if (lane == 0)
-		for (int i = 0; i < 16; i++) atomicAdd(&g_mbik_prof[i], (unsigned long long)pfa[i]);
+		for (int i = 0; i < 24; i++) atomicAdd(&g_mbik_prof[i], (unsigned long long)pfa[i]);
 #endif
 }
 
@@ -1234,8 +1284,8 @@ int32_t mbik_solve_host(mbik_plan *p, int32_t first, int32_t count, const float 
 
 #ifdef MBIK_PROF
 extern "C" int mbik_debug_prof(unsigned long long *out) {
-	if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mbik_prof), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
-	unsigned long long z[16] = {};
+	if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mbik_prof), sizeof(unsigned long long) * 24) != hipSuccess) return -1;
+	unsigned long long z[24] = {};
 	return hipMemcpyToSymbol(HIP_SYMBOL(g_mbik_prof), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
 #endif

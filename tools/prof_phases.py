@@ -8,11 +8,11 @@ from many_bone_ik_amd import _lib, workloads as W
 from many_bone_ik_amd.solver import Plan
 
 NAMES = ["load", "headings_qcp", "clamp_slerp_rotate", "swing", "twist", "global_pass", "store", "total",
-         "step_start", "eff_headings", "qcp_adjugate", "convert_clamp", "slerp", "translate_steps", "qcp_centroid_sums"]
+         "step_start", "eff_headings", "qcp_adjugate", "convert_clamp", "slerp", "translate_steps", "qcp_centroid_sums", "tr_headings_build", "tr_staged_sums", "tr_rotate"]
 dev = torch.device('cuda', 0)
 L = _lib.load()
 L.mbik_debug_prof.argtypes = [C.c_void_p]
-buf = (C.c_ulonglong * 16)()
+buf = (C.c_ulonglong * 24)()
 for case in sys.argv[1:]:
     cfg, n, lanes = (int(x) for x in case.split(':'))
     wl = W.generate(cfg, n)
