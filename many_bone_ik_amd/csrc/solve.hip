@@ -131,9 +131,22 @@ __device__ __forceinline__ Q clamp_cos_half(Q q, double c) {
 
 // Basis::slerp(to, 0) as called with the un-forwarded iteration counters
 // (ik_bone_segment_3d.cpp:148-151): a Basis->Quaternion->Basis round trip, rows rescaled.
-__device__ __forceinline__ B3 slerp_weight0(const B3 &from_b, const B3 &to_b) {
+// The p_to side (its quaternion and row lengths) depends only on the bone's global pose at
+// the start of the step, so callers compute it early, off the critical path.
+struct SlerpTo {
+	Q q;
+	float len[3];
+};
+__device__ __forceinline__ SlerpTo slerp_to(const B3 &to_b) {
+	SlerpTo r;
+	r.q = get_quaternion(to_b);
+#pragma unroll
+	for (int i = 0; i < 3; i++) r.len[i] = length(to_b.r[i]);
+	return r;
+}
+__device__ __forceinline__ B3 slerp_weight0(const B3 &from_b, const SlerpTo &tt) {
 	Q from = get_quaternion(from_b);
-	Q to = get_quaternion(to_b);
+	Q to = tt.q;
 	float cosom = dot(from, to);
 	Q to1 = to;
 	if (cosom < 0.0f) {
@@ -158,7 +171,7 @@ __device__ __forceinline__ B3 slerp_weight0(const B3 &from_b, const B3 &to_b) {
 	B3 b = from_quat(qs);
 #pragma unroll
 	for (int i = 0; i < 3; i++) {
-		float la = length(from_b.r[i]), lb = length(to_b.r[i]);
+		float la = length(from_b.r[i]), lb = tt.len[i];
 		b.r[i] = b.r[i] * (la + (lb - la) * 0.0f);
 	}
 	return b;
@@ -430,6 +443,7 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, size_t
 	const int oe_mode = stab ? (attempt == 0 ? 1 : 2) : 0;
 	X3 Lb = ld_x(L + 12 * b);
 	const X3 Gb = hasP ? P * Lb : Lb;
+	const SlerpTo sto = slerp_to(Gb.b);
 	const bool translate = (t.seg_flags[seg] & mbik::SF_TRANSLATE) != 0;
 	const int e0 = t.seg_eff_off[seg], e1 = t.seg_eff_off[seg + 1];
 	const int nh = t.seg_nh[seg];
@@ -696,7 +710,7 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, size_t
 	MBIK_PROF_T(pc0);
 	MBIK_PROF_ADD(11, pt1, pc0);
 #ifndef MBIK_ABLATE_SLERP
-	rot = slerp_weight0(rot, Gb.b);
+	rot = slerp_weight0(rot, sto);
 #endif
 	MBIK_PROF_T(pc1);
 	MBIK_PROF_ADD(12, pc0, pc1);
