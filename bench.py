@@ -41,6 +41,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--no-autotune", action="store_true", help="keep the plan's automatic launch layout")
     ap.add_argument("--traffic-json", default=os.path.join(HERE, "profiles", "traffic.json"))
     return ap.parse_args()
 
@@ -102,6 +103,11 @@ def main():
     def step():
         plan.solve(pose_in.data_ptr(), targets.data_ptr(), pose_out.data_ptr(), 0, n, stream.cuda_stream)
 
+    if not args.no_autotune:
+        # mbik_plan_autotune: times the candidate launch layouts on this very batch and keeps
+        # the fastest (every layout computes identical bits); part of warmup, not timed.
+        plan.autotune(pose_in.data_ptr(), targets.data_ptr(), pose_out.data_ptr(), 0, n, stream.cuda_stream)
+        info = plan.info()
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
@@ -203,6 +209,7 @@ def main():
                    "skeletons_per_gpu": n, "bones": wl.bone_count, "effectors": int(wl.topo.pins.shape[0]),
                    "cones_per_bone": wl.topo.cones_per_bone, "iterations": wl.topo.iterations,
                    "lanes_per_skeleton": info["lanes_per_skeleton"], "skeletons_per_block": info["skeletons_per_block"],
+                   "lds_bytes_per_block": info["lds_bytes_per_block"],
                    "parallelism": f"dp{world} (skeleton shards, no data-path collective)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

@@ -102,6 +102,7 @@ typedef struct mbik_plan_info {
 	int64_t device_bytes;              /* per-skeleton plan tables resident in HBM */
 	double algorithmic_bytes_per_skeleton; /* pose in/out + targets + plan tables read once */
 	double algorithmic_flops_per_skeleton; /* SURVEY.md §8(d) per-bone-step formula x bone-steps x iterations */
+	int64_t lds_bytes_per_block;       /* LDS of one launch block (spw skeletons + topology tables) */
 } mbik_plan_info;
 
 /* Builds the per-topology tables and the per-skeleton setup data for skeletons
@@ -113,6 +114,18 @@ void mbik_plan_destroy(mbik_plan *plan);
 int32_t mbik_plan_get_info(const mbik_plan *plan, mbik_plan_info *out);
 /* Launch-shape override (0 = automatic).  lanes_per_skeleton must be a power of two <= 64. */
 int32_t mbik_plan_set_launch(mbik_plan *plan, int32_t lanes_per_skeleton);
+/* Full layout override, each 0 = automatic: lanes per skeleton (power of two <= 64),
+ * skeletons per block (<= 64 / lanes), and the checkpoint interval of the iteration-start
+ * globals kept in LDS (1 = every bone; n = every n-th bone of a segment from its root, plus
+ * the parents of segment roots).  Results do not depend on the layout. */
+int32_t mbik_plan_set_layout(mbik_plan *plan, int32_t lanes_per_skeleton, int32_t skeletons_per_block,
+		int32_t global_checkpoint_interval);
+/* Times candidate layouts (checkpoint interval x skeletons per block) on a real batch and
+ * keeps the fastest as the plan's layout.  Runs the solve several times into pose_out
+ * (identical results); synchronizes hip_stream.  The chosen layout is fixed afterwards;
+ * mbik_plan_set_layout(plan, 0, 0, 0) returns to the automatic one. */
+int32_t mbik_plan_autotune(mbik_plan *plan, int32_t first, int32_t count, const float *pose_in, const float *targets,
+		float *pose_out, void *hip_stream);
 
 /* One frame for skeletons [first, first+count): device pointers (hipMalloc'd, on the
  * plan's device), asynchronous on hip_stream (NULL = default stream).  pose_in, targets

@@ -19,7 +19,8 @@ MBIK_EUNSUPPORTED = -4
 MBIK_ENODEV = -5
 
 EXPORTED_SYMBOLS = (
-    "mbik_plan_create", "mbik_plan_destroy", "mbik_plan_get_info", "mbik_plan_set_launch",
+    "mbik_plan_create", "mbik_plan_destroy", "mbik_plan_get_info", "mbik_plan_set_launch", "mbik_plan_set_layout",
+    "mbik_plan_autotune",
     "mbik_solve", "mbik_solve_host", "mbik_segment_solve", "mbik_plan_segment_table", "mbik_describe_topology",
     "mbik_last_error",
 )
@@ -53,7 +54,7 @@ class MbikPlanInfo(C.Structure):
                 ("lanes_per_skeleton", C.c_int32), ("skeletons_per_block", C.c_int32),
                 ("max_headings", C.c_int32), ("device", C.c_int32), ("device_bytes", C.c_int64),
                 ("algorithmic_bytes_per_skeleton", C.c_double),
-                ("algorithmic_flops_per_skeleton", C.c_double)]
+                ("algorithmic_flops_per_skeleton", C.c_double), ("lds_bytes_per_block", C.c_int64)]
 
 
 class MbikError(RuntimeError):
@@ -91,6 +92,10 @@ def load():
     L.mbik_plan_get_info.restype = C.c_int32
     L.mbik_plan_set_launch.argtypes = [vp, C.c_int32]
     L.mbik_plan_set_launch.restype = C.c_int32
+    L.mbik_plan_set_layout.argtypes = [vp, C.c_int32, C.c_int32, C.c_int32]
+    L.mbik_plan_set_layout.restype = C.c_int32
+    L.mbik_plan_autotune.argtypes = [vp, C.c_int32, C.c_int32, vp, vp, vp, vp]
+    L.mbik_plan_autotune.restype = C.c_int32
     L.mbik_solve.argtypes = [vp, C.c_int32, C.c_int32, vp, vp, vp, vp]
     L.mbik_solve.restype = C.c_int32
     L.mbik_solve_host.argtypes = [vp, C.c_int32, C.c_int32, vp, vp, vp]

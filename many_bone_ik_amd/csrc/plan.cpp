@@ -289,22 +289,7 @@ std::string build_topology(const mbik_skeleton_desc &desc, const mbik_config &cf
 	p.seg_height.assign(p.NS, 0);
 	for (int i = 0; i < p.NS; i++)
 		for (int c : p.seg_children[i]) p.seg_height[i] = std::max(p.seg_height[i], p.seg_height[c] + 1);
-	// Staged-heading LDS area (solve.hip, segments solved by several lanes): 12 floats per
-	// heading plus 24 for the exchanged sums.  Segments of one height run concurrently, so
-	// their areas are disjoint; offsets restart at every height.
-	{
-		int maxh = 0;
-		for (int i = 0; i < p.NS; i++) maxh = std::max(maxh, p.seg_height[i]);
-		std::vector<int> used(maxh + 1, 0);
-		p.seg_hbase.assign(p.NS, 0);
-		for (int i = 0; i < p.NS; i++) {
-			if (p.seg_nh[i] < 2) continue;
-			p.seg_hbase[i] = used[p.seg_height[i]];
-			used[p.seg_height[i]] += 12 * p.seg_nh[i] + 24;
-		}
-		p.hs_floats = 0;
-		for (int u : used) p.hs_floats = std::max(p.hs_floats, u);
-	}
+	p.seg_hbase.assign(p.NS, 0); // laid out by build_schedule
 	p.seg_tin.assign(p.NS, 0);
 	p.seg_tout.assign(p.NS, 0);
 	for (int i = 0; i < p.NS; i++) { // post-order: subtree of i = [tin, i]
@@ -579,7 +564,7 @@ std::string build_skeletons(HostPlan &p, int32_t n, const float *setup_pose, con
 // Launch shape + sibling-level schedule
 // ---------------------------------------------------------------------------------------
 int32_t lds_floats_per_skeleton(const HostPlan &p) {
-	return p.B * 24 + p.P * 25 + p.hs_floats + (p.stabilization_passes > 0 ? p.P * 10 : 0);
+	return p.B * 12 + p.n_gck * 12 + p.P * 25 + p.hs_floats + (p.stabilization_passes > 0 ? p.P * 10 : 0);
 }
 
 // Upper bound of the LDS bytes taken by the topology blob (solve.hip: upload_topology).
@@ -590,7 +575,7 @@ int64_t topology_bytes(const HostPlan &p) {
 	ints(p.bone_cons.size()); ints(p.bone_child_eff_off.size()); ints(p.bone_child_effs.size());
 	ints(p.seg_bone_off.size()); ints(p.seg_bones.size()); ints(p.seg_eff_off.size()); ints(p.seg_effs.size());
 	ints(p.seg_eff_hoff.size()); ints(p.seg_nh.size()); ints(p.seg_flags.size()); ints(p.seg_hw_off.size());
-	ints(p.seg_wsum2.size()); ints(p.seg_hbase.size());
+	ints(p.seg_wsum2.size()); ints(p.seg_hbase.size()); ints(p.B); ints(p.seg_bones.size());
 	ints(p.eff_bone.size()); ints(p.eff_path_off.size()); ints(p.eff_path.size()); ints(p.eff_prio.size());
 	ints(p.cons_ncones.size()); ints(2 * p.seg_hw.size()); ints(2 * p.seg_cos_half_damp.size());
 	return (w + 4) * 4;
@@ -602,7 +587,7 @@ static int ceil_log2(int v) {
 	return l;
 }
 
-void build_schedule(HostPlan &p, int32_t lanes, int64_t nlaunch) {
+void build_schedule(HostPlan &p, int32_t lanes, int64_t nlaunch, int32_t spw_override, int32_t interval_override) {
 	int maxh = 0;
 	for (int i = 0; i < p.NS; i++) maxh = std::max(maxh, p.seg_height[i]);
 	std::vector<std::vector<int>> lev(maxh + 1);
@@ -619,7 +604,6 @@ void build_schedule(HostPlan &p, int32_t lanes, int64_t nlaunch) {
 		// level's width is the fastest lane count for C2-C5, also where it leaves the chip
 		// with fewer than one wave per SIMD.
 		K = std::min(64, 1 << ceil_log2(widest));
-		(void)nlaunch;
 	}
 	K = std::max(1, std::min(64, K));
 	p.K = K;
@@ -637,9 +621,92 @@ void build_schedule(HostPlan &p, int32_t lanes, int64_t nlaunch) {
 			p.nrows++;
 		}
 	}
-	p.spw = 64 / K;
+	// Staged-heading LDS area (solve.hip, segments solved by several lanes of a row): 12
+	// floats per heading plus 24 for the exchanged sums.  The segments of one row run
+	// concurrently, so their areas are disjoint; offsets restart at every row.
+	p.seg_hbase.assign(p.NS, 0);
+	p.hs_floats = 0;
+	for (int r = 0; r < p.nrows; r++) {
+		int used = 0;
+		for (int l = 0; l < K; l++) {
+			const SchedTask &tk = p.sched[(size_t)r * K + l];
+			if (tk.seg < 0 || tk.j != 0 || tk.m < 2 || p.seg_nh[tk.seg] < 2) continue;
+			p.seg_hbase[tk.seg] = used;
+			used += 12 * p.seg_nh[tk.seg] + 24;
+		}
+		p.hs_floats = std::max(p.hs_floats, used);
+	}
+	// Skeletons per block and the checkpoint interval of the iteration-start globals.  LDS
+	// (160 KiB per CU) bounds how many skeletons a CU holds at once; a block's LDS is spw
+	// skeletons plus one copy of the topology blob.  A launch that fits the chip at the full
+	// 64 / K per wave with every global kept keeps that (a chain of skeletons is
+	// latency-bound, so fewer waves of full width cost nothing).  A larger launch takes the
+	// (interval, spw) with the most skeletons resident per CU, discounted by what sparser
+	// checkpoints cost in recomputed products and LDS traffic (factors from tools/layout_sweep.py
+	// on MI355X: interval 2 ~3 %, no interior checkpoints ~35 % per wave; mbik_plan_autotune
+	// measures instead of modelling).
 	const int64_t topo = topology_bytes(p);
-	while (p.spw > 1 && (int64_t)p.spw * ((lds_floats_per_skeleton(p) + 3) & ~3) * 4 + topo > 160 * 1024) p.spw /= 2;
+	constexpr int64_t kCUs = 256;
+	auto set_interval = [&](int c) -> double {
+		p.g_interval = c;
+		p.bone_gslot.assign(p.B, -1);
+		for (int sg = 0; sg < p.NS; sg++) {
+			const int k0 = p.seg_bone_off[sg], k1 = p.seg_bone_off[sg + 1];
+			for (int k = k0; k < k1; k++)
+				if ((k1 - 1 - k) % c == 0) p.bone_gslot[p.seg_bones[k]] = 0;
+			const int pp = p.bone_pose_parent[p.seg_bones[k1 - 1]];
+			if (pp >= 0) p.bone_gslot[pp] = 0;
+		}
+		p.n_gck = 0;
+		for (int b = 0; b < p.B; b++)
+			if (p.bone_gslot[b] >= 0) p.bone_gslot[b] = p.n_gck++;
+		p.seg_anchor.assign(p.seg_bones.size(), -1);
+		int64_t extra = 0;
+		for (int sg = 0; sg < p.NS; sg++) {
+			const int k0 = p.seg_bone_off[sg], k1 = p.seg_bone_off[sg + 1];
+			for (int k = k0; k < k1 - 1; k++) {
+				int kc = k + 1;
+				while (p.bone_gslot[p.seg_bones[kc]] < 0) kc++; // ends at the segment root
+				p.seg_anchor[k] = kc;
+				extra += kc - (k + 1);
+			}
+		}
+		return p.seg_bones.empty() ? 0.0 : (double)extra / (double)p.seg_bones.size();
+	};
+	auto resident = [&](int spw) -> int64_t {
+		const int64_t block = spw * (int64_t)(((lds_floats_per_skeleton(p) + 3) & ~3) * 4) + topo;
+		return block > 160 * 1024 ? 0 : (160 * 1024 / block) * spw;
+	};
+	set_interval(interval_override > 0 ? interval_override : 1);
+	int best = 64 / K;
+	while (best > 1 && resident(best) == 0) best--;
+	int best_c = interval_override > 0 ? interval_override : 1;
+	if (spw_override > 0) {
+		best = std::min(spw_override, 64 / K);
+		while (best > 1 && resident(best) == 0) best--;
+	} else if (resident(best) * kCUs < nlaunch) {
+		double best_score = -1.0;
+		std::vector<int> cands = interval_override > 0 ? std::vector<int>{interval_override} : std::vector<int>{1, 2, 1 << 20};
+		for (int c : cands) {
+			set_interval(c);
+			const double factor = c == 1 ? 1.0 : (c == 2 ? 0.97 : 0.65);
+			for (int spw = 1; spw <= 64 / K; spw++) {
+				const int64_t res = resident(spw);
+				if (res == 0) continue;
+				const int64_t blocks = res / spw;
+				// more than ~4 single-wave blocks per CU share SIMDs (issue-bound)
+				const double score = (double)res * factor * std::min(1.0, 4.0 / (double)blocks);
+				if (score >= best_score) {
+					best_score = score;
+					best = spw;
+					best_c = c;
+				}
+			}
+		}
+	}
+	set_interval(best_c);
+	p.spw = best;
+	p.lds_block_bytes = best * (int64_t)(((lds_floats_per_skeleton(p) + 3) & ~3) * 4) + topo;
 }
 
 } // namespace mbik

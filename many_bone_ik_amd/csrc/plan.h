@@ -78,6 +78,13 @@ struct HostPlan {
 	int32_t max_headings = 0;
 	// ---- launch shape ----
 	int32_t K = 4, log2K = 2, spw = 16;
+	int64_t lds_block_bytes = 0;
+	// Iteration-start globals kept in LDS only for checkpoint bones: every g_interval-th bone
+	// of a segment counted from its root (the root included) and every parent of a segment
+	// root; a bone-step rebuilds its parent's global from the nearest checkpoint above it.
+	int32_t g_interval = 1, n_gck = 0;
+	std::vector<int32_t> bone_gslot;                // LDS slot of a checkpoint bone, else -1
+	std::vector<int32_t> seg_anchor;                // per seg_bones index: the checkpoint's index, -1 = parent outside
 	std::vector<SchedTask> sched;                   // [nrows][K]
 	int32_t nrows = 0;
 	// ---- per skeleton, SoA [item][field][N] ----
@@ -96,8 +103,10 @@ std::string build_topology(const mbik_skeleton_desc &desc, const mbik_config &cf
 std::string build_skeletons(HostPlan &plan, int32_t n, const float *setup_pose, const float *cones, const float *twist,
 		int32_t max_cones_in);
 // Chooses lanes-per-skeleton / skeletons-per-block and the sibling-level schedule.
-void build_schedule(HostPlan &plan, int32_t lanes_per_skeleton, int64_t skeletons_in_launch);
-// LDS floats per skeleton used by the kernel: L, G (12 per bone), targets + stale cache
+// spw_override / interval_override: 0 = automatic (mbik_plan_set_layout).
+void build_schedule(HostPlan &plan, int32_t lanes_per_skeleton, int64_t skeletons_in_launch, int32_t spw_override = 0,
+		int32_t interval_override = 0);
+// LDS floats per skeleton used by the kernel: L (12 per bone), G (12 per checkpoint), targets + stale cache
 // (12 + 12 per pin), stale flags (1 per pin), the staged-heading area (hs_floats), and with
 // stabilization the pre-loop target
 // origins (3 per pin) and the manual-MSD terms (7 per pin).

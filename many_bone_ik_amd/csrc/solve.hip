@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <tuple>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -64,13 +65,14 @@ namespace {
 	X(int, bone_child_eff_off) X(int, bone_child_effs) X(int, seg_bone_off) X(int, seg_bones)         \
 	X(int, seg_eff_off) X(int, seg_effs) X(int, seg_eff_hoff) X(int, seg_nh) X(int, seg_flags)         \
 	X(int, seg_hw_off) X(int, eff_bone) X(int, eff_path_off) X(int, eff_path) X(float, eff_prio)       \
-	X(int, cons_ncones) X(float, seg_wsum2) X(int, seg_hbase) X(double, seg_hw) X(double, seg_cos_half_damp) X(int4, sched)
+	X(int, cons_ncones) X(float, seg_wsum2) X(int, seg_hbase) X(int, bone_gslot) X(int, seg_anchor) X(double, seg_hw) X(double, seg_cos_half_damp) X(int4, sched)
 
 struct DevPlan {
 	int B, P, NS, NC, max_cones, nrows, K, log2K, spw, lds_stride;
 	int N, cf_stride, cd_stride;
 	int stab;            // stabilization_passes (root segments only, SF_STAB)
 	int hs_floats;       // staged-heading LDS floats per skeleton
+	int n_gck;           // checkpoint globals per skeleton (HostPlan::bone_gslot)
 	int constraint_mode; // ManyBoneIK3D::constraint_mode
 	int topo_words; // blob size in 32-bit words (multiple of 4)
 	const uint4 *topo_blob;
@@ -435,7 +437,18 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, size_t
 	const int b = t.seg_bones[k];
 	const int pp = t.bone_pose_parent[b];
 	const bool hasP = pp != mbik::POSE_PARENT_NONE;
-	const X3 P = pp >= 0 ? ld_x(G + 12 * pp) : xid();
+	// The parent's iteration-start global: stored if the parent is a checkpoint, else rebuilt
+	// from the nearest checkpoint above it, with the global pass's own products.
+	X3 P = xid();
+	if (pp >= 0) {
+		const int kc = t.seg_anchor[k];
+		if (kc < 0) {
+			P = ld_x(G + 12 * t.bone_gslot[pp]);
+		} else {
+			P = ld_x(G + 12 * t.bone_gslot[t.seg_bones[kc]]);
+			for (int q = kc - 1; q > k; q--) P = P * ld_x(L + 12 * t.seg_bones[q]);
+		}
+	}
 	const B3 Pinv = inverse(P.b);
 	const bool stab = STAB && (t.seg_flags[seg] & mbik::SF_STAB) != 0;
 	const X3 Lprev = ld_x(L + 12 * b); // prev_transform (:136)
@@ -863,8 +876,8 @@ __device__ void global_pass(const DevPlan &t, int seg, const float *L, float *G)
 		X3 Lb = ld_x(L + 12 * b);
 		X3 Gb;
 		if (k < t.seg_bone_off[seg + 1] - 1) Gb = Gprev * Lb; // parent = the bone just done
-		else Gb = pp >= 0 ? ld_x(G + 12 * pp) * Lb : (pp == mbik::POSE_PARENT_ORIGIN ? xid() * Lb : Lb);
-		st_x(G + 12 * b, Gb);
+		else Gb = pp >= 0 ? ld_x(G + 12 * t.bone_gslot[pp]) * Lb : (pp == mbik::POSE_PARENT_ORIGIN ? xid() * Lb : Lb);
+		if (t.bone_gslot[b] >= 0) st_x(G + 12 * t.bone_gslot[b], Gb);
 		Gprev = Gb;
 	}
 }
@@ -917,7 +930,7 @@ __global__ __launch_bounds__(64) void mbik_solve_kernel(DevPlan t, int first, in
 	const int B = t.B, P = t.P, K = t.K;
 	float *L = lds + (size_t)g * t.lds_stride;
 	float *G = L + 12 * B;
-	float *TG = G + 12 * B;
+	float *TG = G + 12 * t.n_gck;
 	float *ST = TG + 12 * P;
 	float *HS = ST + 12 * P;                        // staged headings (t.seg_hbase), 16-B aligned
 	int *SF = reinterpret_cast<int *>(HS + t.hs_floats);
@@ -983,13 +996,13 @@ __global__ __launch_bounds__(64) void mbik_solve_kernel(DevPlan t, int first, in
 struct mbik_plan {
 	mbik::HostPlan host;
 	int device = 0;
-	int lanes_override = 0;
+	int lanes_override = 0, spw_override = 0, interval_override = 0;
 	std::vector<void *> allocs;
 	DevPlan dev{};
 	int64_t device_bytes = 0;
 	double alg_bytes = 0;
 	double alg_flops = 0;
-	int sched_K = -1;
+	int sched_K = -1, sched_c = -1; // layout of the uploaded topology blob
 	void *d_sched = nullptr; // topology blob (includes the lane schedule)
 	// scratch for mbik_solve_host
 	float *d_in = nullptr, *d_tg = nullptr, *d_out = nullptr;
@@ -1060,15 +1073,22 @@ int upload_topology(mbik_plan *p) {
 
 int ensure_schedule(mbik_plan *p, int64_t nlaunch) {
 	mbik::HostPlan &h = p->host;
-	mbik::build_schedule(h, p->lanes_override, nlaunch);
-	if (p->sched_K == h.K && p->d_sched) return MBIK_OK;
+	mbik::build_schedule(h, p->lanes_override, nlaunch, p->spw_override, p->interval_override);
+	if (p->sched_K == h.K && p->sched_c == h.g_interval && p->d_sched) {
+		p->dev.spw = h.spw;
+		return MBIK_OK;
+	}
 	int rc = upload_topology(p);
 	if (rc) return rc;
 	p->sched_K = h.K;
+	p->sched_c = h.g_interval;
 	p->dev.nrows = h.nrows;
 	p->dev.K = h.K;
 	p->dev.log2K = h.log2K;
 	p->dev.spw = h.spw;
+	p->dev.hs_floats = h.hs_floats;
+	p->dev.n_gck = h.n_gck;
+	p->dev.lds_stride = (mbik::lds_floats_per_skeleton(h) + 3) & ~3;
 	return MBIK_OK;
 }
 
@@ -1152,6 +1172,7 @@ int32_t mbik_plan_create(const mbik_skeleton_desc *desc, const mbik_config *conf
 	d.B = h.B; d.P = h.P; d.NS = h.NS; d.NC = h.NC; d.max_cones = h.max_cones; d.N = h.N;
 	d.cf_stride = h.cf_stride(); d.cd_stride = h.cd_stride();
 	d.stab = h.stabilization_passes; d.constraint_mode = h.constraint_mode; d.hs_floats = h.hs_floats;
+	d.n_gck = h.n_gck;
 	d.lds_stride = (mbik::lds_floats_per_skeleton(h) + 3) & ~3;
 	int rc = 0;
 	rc = rc ? rc : upload(p.get(), h.D, d.D);
@@ -1230,6 +1251,7 @@ int32_t mbik_plan_get_info(const mbik_plan *p, mbik_plan_info *o) {
 	o->device_bytes = p->device_bytes;
 	o->algorithmic_bytes_per_skeleton = p->alg_bytes;
 	o->algorithmic_flops_per_skeleton = p->alg_flops;
+	o->lds_bytes_per_block = p->host.lds_block_bytes;
 	return MBIK_OK;
 }
 
@@ -1239,6 +1261,71 @@ int32_t mbik_plan_set_launch(mbik_plan *p, int32_t lanes) {
 	p->lanes_override = lanes;
 	p->sched_K = -1;
 	return MBIK_OK;
+}
+
+int32_t mbik_plan_set_layout(mbik_plan *p, int32_t lanes, int32_t skeletons_per_block, int32_t global_checkpoint_interval) {
+	if (!p) return fail(MBIK_EINVAL, "null plan");
+	if (lanes < 0 || lanes > 64 || (lanes & (lanes - 1))) return fail(MBIK_EINVAL, "lanes_per_skeleton must be 0 or a power of two <= 64");
+	if (skeletons_per_block < 0 || skeletons_per_block > 64) return fail(MBIK_EINVAL, "skeletons_per_block must be in [0, 64]");
+	if (global_checkpoint_interval < 0) return fail(MBIK_EINVAL, "global_checkpoint_interval must be >= 0");
+	p->lanes_override = lanes;
+	p->spw_override = skeletons_per_block;
+	p->interval_override = global_checkpoint_interval;
+	p->sched_K = -1;
+	return MBIK_OK;
+}
+
+int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const float *pose_in, const float *targets,
+		float *pose_out, void *hip_stream) {
+	if (!p) return fail(MBIK_EINVAL, "null plan");
+	if (count <= 0) return MBIK_OK;
+	DeviceGuard guard(p->device);
+	hipStream_t st = reinterpret_cast<hipStream_t>(hip_stream);
+	const int lanes = p->lanes_override;
+	// Candidate layouts: checkpoint interval x {the interval's residency-best spw, full 64/K}.
+	// Every layout computes the same bits; only the time differs.
+	std::vector<std::pair<int, int>> cands; // (spw override, interval)
+	for (int c : {1, 2, 4, 1 << 20}) {
+		cands.push_back({0, c});
+		cands.push_back({64, c});
+	}
+	hipEvent_t e0, e1;
+	if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return fail(MBIK_EHIP, "hipEventCreate");
+	float best_ms = 0.0f;
+	int best_spw = 0, best_c = 0, rc = MBIK_OK;
+	std::vector<std::tuple<int, int, int>> seen; // resolved (K, spw, interval)
+	for (auto [spw, c] : cands) {
+		p->spw_override = spw;
+		p->interval_override = c;
+		p->lanes_override = lanes;
+		if ((rc = ensure_schedule(p, count)) != MBIK_OK) break;
+		const auto key = std::make_tuple(p->host.K, p->host.spw, p->host.g_interval);
+		if (std::find(seen.begin(), seen.end(), key) != seen.end()) continue;
+		seen.push_back(key);
+		if ((rc = launch(p, first, count, pose_in, targets, pose_out, st, p->host.iterations, 0, p->host.NS - 1)) != MBIK_OK) break;
+		(void)hipEventRecord(e0, st);
+		for (int r = 0; r < 2 && rc == MBIK_OK; r++)
+			rc = launch(p, first, count, pose_in, targets, pose_out, st, p->host.iterations, 0, p->host.NS - 1);
+		if (rc != MBIK_OK) break;
+		(void)hipEventRecord(e1, st);
+		if (hipEventSynchronize(e1) != hipSuccess) {
+			rc = fail(MBIK_EHIP, "hipEventSynchronize");
+			break;
+		}
+		float ms = 0.0f;
+		(void)hipEventElapsedTime(&ms, e0, e1);
+		if (best_c == 0 || ms < best_ms) {
+			best_ms = ms;
+			best_spw = p->host.spw;
+			best_c = p->host.g_interval;
+		}
+	}
+	(void)hipEventDestroy(e0);
+	(void)hipEventDestroy(e1);
+	if (rc != MBIK_OK) return rc;
+	p->spw_override = best_spw;
+	p->interval_override = best_c;
+	return ensure_schedule(p, count);
 }
 
 int32_t mbik_solve(mbik_plan *p, int32_t first, int32_t count, const float *pose_in, const float *targets, float *pose_out,

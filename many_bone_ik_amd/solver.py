@@ -115,6 +115,18 @@ class Plan:
     def set_launch(self, lanes: int):
         check(self._L.mbik_plan_set_launch(self.h, int(lanes)))
 
+    def set_layout(self, lanes: int = 0, skeletons_per_block: int = 0, global_checkpoint_interval: int = 0):
+        """Launch layout override (0 = automatic); results do not depend on it."""
+        check(self._L.mbik_plan_set_layout(self.h, int(lanes), int(skeletons_per_block),
+                                           int(global_checkpoint_interval)))
+
+    def autotune(self, pose_in_ptr: int, targets_ptr: int, pose_out_ptr: int, first: int = 0,
+                 count: int | None = None, stream: int = 0):
+        """mbik_plan_autotune: time candidate layouts on this batch, keep the fastest."""
+        count = self.n - first if count is None else count
+        check(self._L.mbik_plan_autotune(self.h, first, count, C.c_void_p(pose_in_ptr), C.c_void_p(targets_ptr),
+                                         C.c_void_p(pose_out_ptr), C.c_void_p(stream or None)))
+
     def solve(self, pose_in_ptr: int, targets_ptr: int, pose_out_ptr: int, first: int = 0, count: int | None = None,
               stream: int = 0):
         count = self.n - first if count is None else count

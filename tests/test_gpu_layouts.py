@@ -1,0 +1,78 @@
+"""Results do not depend on the launch layout (mbik_plan_set_layout): lanes per skeleton,
+skeletons per block and the checkpoint interval of the iteration-start globals kept in
+LDS.  Every layout is bitwise equal to the oracle.  Needs an MI355X: -m gpu."""
+import numpy as np
+import pytest
+
+from many_bone_ik_amd import _lib
+from many_bone_ik_amd import workloads as W
+from many_bone_ik_amd.solver import Plan
+
+from .test_gpu_parity import assert_parity
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("cfg,n", [(1, 8), (2, 48), (3, 48), (4, 16), (5, 6)])
+@pytest.mark.parametrize("interval", [2, 3, 1 << 20])
+@pytest.mark.parametrize("lanes,spw", [(0, 0), (0, 3), (4, 0), (1, 5)])
+def test_layouts_bitwise_vs_oracle(oracle, mbik, cfg, n, interval, lanes, spw):
+    wl = W.generate(cfg, n, first=5000)
+    ref = oracle.Oracle(wl).solve(wl.pose, wl.targets, threads=8)
+    plan = Plan.from_workload(wl)
+    plan.set_layout(lanes, spw, interval)
+    got = plan.solve_host(wl.pose, wl.targets)
+    info = plan.info()
+    assert spw == 0 or info["skeletons_per_block"] <= spw
+    assert_parity(got, ref, f"C{cfg} interval={interval} lanes={lanes} spw={spw}")
+
+
+def test_layout_with_stabilization(oracle, mbik):
+    wl = W.generate(1, 16, first=77)
+    ref = oracle.Oracle(wl, stabilization_passes=2).solve(wl.pose, wl.targets, threads=8)
+    plan = Plan.from_workload(wl, stabilization_passes=2)
+    plan.set_layout(0, 7, 3)
+    assert_parity(plan.solve_host(wl.pose, wl.targets), ref, "C1 stab interval=3")
+
+
+def test_auto_layout_of_a_large_launch_is_exact(oracle, mbik):
+    """A launch larger than the chip holds switches to the residency layout; spot-check it."""
+    import torch
+    wl = W.generate(5, 16384)
+    plan = Plan.from_workload(wl)
+    dev = torch.device("cuda", 0)
+    pi = torch.from_numpy(wl.pose).to(dev)
+    tg = torch.from_numpy(wl.targets).to(dev)
+    po = torch.empty_like(pi)
+    plan.solve(pi.data_ptr(), tg.data_ptr(), po.data_ptr(), 0, wl.n, torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize()
+    got = po.cpu().numpy()
+    for first in (0, 8191, 16380):
+        sub = W.generate(5, 4, first=first)
+        ref = oracle.Oracle(sub).solve(sub.pose, sub.targets, threads=8)
+        assert_parity(got[first:first + 4], ref, f"C5 auto layout @{first}")
+
+
+def test_layout_argument_checks(mbik):
+    wl = W.generate(3, 2)
+    plan = Plan.from_workload(wl)
+    for args in [(3, 0, 0), (0, 65, 0), (0, 0, -1)]:
+        with pytest.raises(_lib.MbikError) as e:
+            plan.set_layout(*args)
+        assert e.value.code == _lib.MBIK_EINVAL
+
+
+def test_autotune_keeps_results(oracle, mbik):
+    import torch
+    wl = W.generate(2, 512, first=9000)
+    plan = Plan.from_workload(wl)
+    dev = torch.device("cuda", 0)
+    pi = torch.from_numpy(wl.pose).to(dev)
+    tg = torch.from_numpy(wl.targets).to(dev)
+    po = torch.empty_like(pi)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    plan.autotune(pi.data_ptr(), tg.data_ptr(), po.data_ptr(), stream=st)
+    plan.solve(pi.data_ptr(), tg.data_ptr(), po.data_ptr(), stream=st)
+    torch.cuda.synchronize()
+    ref = oracle.Oracle(wl).solve(wl.pose, wl.targets, threads=8)
+    assert_parity(po.cpu().numpy(), ref, "C2 after autotune")

@@ -1,0 +1,31 @@
+"""Time mbik_solve under explicit layouts: args cfg:n:lanes:spw:interval (0 = auto)."""
+import sys, json
+import torch
+sys.path.insert(0, '.')
+from many_bone_ik_amd import workloads as W
+from many_bone_ik_amd.solver import Plan
+
+dev = torch.device('cuda', 0)
+cache = {}
+for arg in sys.argv[1:]:
+    cfg, n, lanes, spw, interval = (int(x) for x in arg.split(':'))
+    if (cfg, n) not in cache:
+        cache.clear()
+        cache[(cfg, n)] = W.generate(cfg, n)
+    wl = cache[(cfg, n)]
+    p = Plan.from_workload(wl)
+    p.set_layout(lanes, spw, interval)
+    pi = torch.from_numpy(wl.pose).to(dev); tg = torch.from_numpy(wl.targets).to(dev); po = torch.empty_like(pi)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    p.solve(pi.data_ptr(), tg.data_ptr(), po.data_ptr(), 0, n, st); torch.cuda.synchronize()
+    e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
+    reps = 5
+    e0.record()
+    for _ in range(reps):
+        p.solve(pi.data_ptr(), tg.data_ptr(), po.data_ptr(), 0, n, st)
+    e1.record(); torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    inf = p.info()
+    print(json.dumps(dict(arg=arg, lanes=inf['lanes_per_skeleton'], spw=inf['skeletons_per_block'],
+                          lds=inf['lds_bytes_per_block'], ms=round(ms, 3), mskel_s=round(n / ms / 1e3, 3))), flush=True)
+    p.close()

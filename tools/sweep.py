@@ -32,6 +32,6 @@ for case in cases:
         e1.record(); torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / reps
         inf = p.info()
-        print(json.dumps(dict(cfg=cfg, n=n, lanes=inf['lanes_per_skeleton'], spw=inf['skeletons_per_block'], ms=round(ms, 3),
+        print(json.dumps(dict(cfg=cfg, n=n, lanes=inf["lanes_per_skeleton"], spw=inf["skeletons_per_block"], lds=inf["lds_bytes_per_block"], ms=round(ms, 3),
                               mskel_s=round(n / ms / 1e3, 3))), flush=True)
         p.close()
