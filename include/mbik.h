@@ -120,6 +120,9 @@ int32_t mbik_plan_set_launch(mbik_plan *plan, int32_t lanes_per_skeleton);
  * the parents of segment roots).  Results do not depend on the layout. */
 int32_t mbik_plan_set_layout(mbik_plan *plan, int32_t lanes_per_skeleton, int32_t skeletons_per_block,
 		int32_t global_checkpoint_interval);
+/* Diagnostic: how many one-wave blocks using lds_bytes_per_block of LDS one CU of the plan's
+ * device holds at once (the runtime occupancy query for the plan's kernel). */
+int32_t mbik_plan_resident_blocks(const mbik_plan *plan, int64_t lds_bytes_per_block);
 /* Times candidate layouts (checkpoint interval x skeletons per block) on a real batch and
  * keeps the fastest as the plan's layout.  Runs the solve several times into pose_out
  * (identical results); synchronizes hip_stream.  The chosen layout is fixed afterwards;

@@ -587,7 +587,8 @@ static int ceil_log2(int v) {
 	return l;
 }
 
-void build_schedule(HostPlan &p, int32_t lanes, int64_t nlaunch, int32_t spw_override, int32_t interval_override) {
+void build_schedule(HostPlan &p, int32_t lanes, int64_t nlaunch, int32_t spw_override, int32_t interval_override,
+		BlocksPerCU blocks_per_cu, void *ctx, int cus) {
 	int maxh = 0;
 	for (int i = 0; i < p.NS; i++) maxh = std::max(maxh, p.seg_height[i]);
 	std::vector<std::vector<int>> lev(maxh + 1);
@@ -642,11 +643,12 @@ void build_schedule(HostPlan &p, int32_t lanes, int64_t nlaunch, int32_t spw_ove
 	// 64 / K per wave with every global kept keeps that (a chain of skeletons is
 	// latency-bound, so fewer waves of full width cost nothing).  A larger launch takes the
 	// (interval, spw) with the most skeletons resident per CU, discounted by what sparser
-	// checkpoints cost in recomputed products and LDS traffic (factors from tools/layout_sweep.py
-	// on MI355X: interval 2 ~3 %, no interior checkpoints ~35 % per wave; mbik_plan_autotune
-	// measures instead of modelling).
+	// checkpoints cost in recomputed products (per-wave cycles from tools/prof_phases.py on
+	// MI355X: interval 2 ~1.5 %, no interior checkpoints 6-8 %; mbik_plan_autotune measures
+	// instead of modelling).  Residency comes from the runtime's occupancy query (LDS
+	// allocation granularity and the register budget: at most one wave per SIMD).
 	const int64_t topo = topology_bytes(p);
-	constexpr int64_t kCUs = 256;
+	const int64_t kCUs = cus;
 	auto set_interval = [&](int c) -> double {
 		p.g_interval = c;
 		p.bone_gslot.assign(p.B, -1);
@@ -675,7 +677,9 @@ void build_schedule(HostPlan &p, int32_t lanes, int64_t nlaunch, int32_t spw_ove
 	};
 	auto resident = [&](int spw) -> int64_t {
 		const int64_t block = spw * (int64_t)(((lds_floats_per_skeleton(p) + 3) & ~3) * 4) + topo;
-		return block > 160 * 1024 ? 0 : (160 * 1024 / block) * spw;
+		if (block > 160 * 1024) return 0;
+		const int64_t blocks = blocks_per_cu ? blocks_per_cu(ctx, block) : 160 * 1024 / block;
+		return blocks * spw;
 	};
 	set_interval(interval_override > 0 ? interval_override : 1);
 	int best = 64 / K;
@@ -689,7 +693,7 @@ void build_schedule(HostPlan &p, int32_t lanes, int64_t nlaunch, int32_t spw_ove
 		std::vector<int> cands = interval_override > 0 ? std::vector<int>{interval_override} : std::vector<int>{1, 2, 1 << 20};
 		for (int c : cands) {
 			set_interval(c);
-			const double factor = c == 1 ? 1.0 : (c == 2 ? 0.97 : 0.65);
+			const double factor = c == 1 ? 1.0 : (c == 2 ? 0.985 : 0.92);
 			for (int spw = 1; spw <= 64 / K; spw++) {
 				const int64_t res = resident(spw);
 				if (res == 0) continue;

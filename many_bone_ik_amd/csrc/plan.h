@@ -104,8 +104,11 @@ std::string build_skeletons(HostPlan &plan, int32_t n, const float *setup_pose, 
 		int32_t max_cones_in);
 // Chooses lanes-per-skeleton / skeletons-per-block and the sibling-level schedule.
 // spw_override / interval_override: 0 = automatic (mbik_plan_set_layout).
+// blocks_per_cu(lds_bytes): how many one-wave blocks of that LDS size a CU holds at once
+// (the device's occupancy query); nullptr = LDS-only estimate.  cus: compute units.
+using BlocksPerCU = int (*)(void *ctx, int64_t lds_bytes);
 void build_schedule(HostPlan &plan, int32_t lanes_per_skeleton, int64_t skeletons_in_launch, int32_t spw_override = 0,
-		int32_t interval_override = 0);
+		int32_t interval_override = 0, BlocksPerCU blocks_per_cu = nullptr, void *ctx = nullptr, int cus = 256);
 // LDS floats per skeleton used by the kernel: L (12 per bone), G (12 per checkpoint), targets + stale cache
 // (12 + 12 per pin), stale flags (1 per pin), the staged-heading area (hs_floats), and with
 // stabilization the pre-loop target

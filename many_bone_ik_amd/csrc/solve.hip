@@ -893,8 +893,13 @@ __device__ void write_pose(const X3 &t, float *out) {
 	out[7] = sc.x; out[8] = sc.y; out[9] = sc.z;
 }
 
+// One wave per block, and LDS caps residency at <= 4 blocks per CU (one wave per SIMD), so
+// the kernel may use the whole register file (MBIK_WAVES_PER_EU 1: up to 512 VGPRs).
+#ifndef MBIK_WAVES_PER_EU
+#define MBIK_WAVES_PER_EU 1
+#endif
 template <bool STAB>
-__global__ __launch_bounds__(64) void mbik_solve_kernel(DevPlan t, int first, int count, const float *__restrict__ pose_in,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MBIK_WAVES_PER_EU, MBIK_WAVES_PER_EU))) void mbik_solve_kernel(DevPlan t, int first, int count, const float *__restrict__ pose_in,
 		const float *__restrict__ targets, float *__restrict__ pose_out, int iterations, int seg_lo, int seg_hi) {
 	extern __shared__ float4 lds4[];
 	const int lane = threadIdx.x;
@@ -997,6 +1002,7 @@ struct mbik_plan {
 	mbik::HostPlan host;
 	int device = 0;
 	int lanes_override = 0, spw_override = 0, interval_override = 0;
+	int cu_count = 256;
 	std::vector<void *> allocs;
 	DevPlan dev{};
 	int64_t device_bytes = 0;
@@ -1071,9 +1077,26 @@ int upload_topology(mbik_plan *p) {
 	return MBIK_OK;
 }
 
+// Resident one-wave blocks per CU for a block's LDS size, from the runtime's occupancy
+// query on the kernel instantiation the plan launches (LDS granularity and registers).
+int blocks_per_cu(void *ctx, int64_t lds_bytes) {
+	const mbik_plan *p = static_cast<const mbik_plan *>(ctx);
+	static std::once_flag once;
+	std::call_once(once, [] {
+		(void)hipFuncSetAttribute((const void *)mbik_solve_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+		(void)hipFuncSetAttribute((const void *)mbik_solve_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+	});
+	int n = 0;
+	const void *k = p->host.stabilization_passes > 0 ? (const void *)mbik_solve_kernel<true> : (const void *)mbik_solve_kernel<false>;
+	if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, 64, (size_t)lds_bytes) != hipSuccess || n <= 0)
+		return (int)(160 * 1024 / std::max<int64_t>(1, lds_bytes));
+	return n;
+}
+
 int ensure_schedule(mbik_plan *p, int64_t nlaunch) {
 	mbik::HostPlan &h = p->host;
-	mbik::build_schedule(h, p->lanes_override, nlaunch, p->spw_override, p->interval_override);
+	mbik::build_schedule(h, p->lanes_override, nlaunch, p->spw_override, p->interval_override, blocks_per_cu, p,
+			p->cu_count);
 	if (p->sched_K == h.K && p->sched_c == h.g_interval && p->d_sched) {
 		p->dev.spw = h.spw;
 		return MBIK_OK;
@@ -1167,6 +1190,11 @@ int32_t mbik_plan_create(const mbik_skeleton_desc *desc, const mbik_config *conf
 			if (p->host.eff_path_off[e + 1] - p->host.eff_path_off[e] > 4096) return fail(MBIK_EUNSUPPORTED, "skeleton too deep");
 		}
 	DeviceGuard guard(device);
+	{
+		int cus = 0;
+		if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+			p->cu_count = cus;
+	}
 	mbik::HostPlan &h = p->host;
 	DevPlan &d = p->dev;
 	d.B = h.B; d.P = h.P; d.NS = h.NS; d.NC = h.NC; d.max_cones = h.max_cones; d.N = h.N;
@@ -1275,6 +1303,12 @@ int32_t mbik_plan_set_layout(mbik_plan *p, int32_t lanes, int32_t skeletons_per_
 	return MBIK_OK;
 }
 
+int32_t mbik_plan_resident_blocks(const mbik_plan *p, int64_t lds_bytes_per_block) {
+	if (!p) return fail(MBIK_EINVAL, "null plan");
+	DeviceGuard guard(p->device);
+	return blocks_per_cu(const_cast<mbik_plan *>(p), lds_bytes_per_block);
+}
+
 int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const float *pose_in, const float *targets,
 		float *pose_out, void *hip_stream) {
 	if (!p) return fail(MBIK_EINVAL, "null plan");
@@ -1282,12 +1316,21 @@ int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const flo
 	DeviceGuard guard(p->device);
 	hipStream_t st = reinterpret_cast<hipStream_t>(hip_stream);
 	const int lanes = p->lanes_override;
-	// Candidate layouts: checkpoint interval x {the interval's residency-best spw, full 64/K}.
-	// Every layout computes the same bits; only the time differs.
+	// Candidate layouts: for each checkpoint interval, the largest skeletons-per-block at each
+	// distinct residency (blocks per CU).  Every layout computes the same bits; only the time
+	// differs.
 	std::vector<std::pair<int, int>> cands; // (spw override, interval)
 	for (int c : {1, 2, 4, 1 << 20}) {
-		cands.push_back({0, c});
-		cands.push_back({64, c});
+		int last_blocks = -1;
+		for (int spw = 64; spw >= 1; spw--) {
+			mbik::build_schedule(p->host, lanes, count, spw, c, blocks_per_cu, p, p->cu_count);
+			if (p->host.spw != spw) continue; // capped by 64 / K or by LDS
+			const int blocks = blocks_per_cu(p, p->host.lds_block_bytes);
+			if (blocks != last_blocks) {
+				cands.push_back({spw, c});
+				last_blocks = blocks;
+			}
+		}
 	}
 	hipEvent_t e0, e1;
 	if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return fail(MBIK_EHIP, "hipEventCreate");

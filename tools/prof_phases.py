@@ -14,9 +14,13 @@ L = _lib.load()
 L.mbik_debug_prof.argtypes = [C.c_void_p]
 buf = (C.c_ulonglong * 24)()
 for case in sys.argv[1:]:
-    cfg, n, lanes = (int(x) for x in case.split(':'))
+    parts = [int(x) for x in case.split(':')]
+    cfg, n, lanes = parts[:3]
+    spw, interval = (parts[3:5] + [0, 0])[:2] if len(parts) > 3 else (0, 0)
     wl = W.generate(cfg, n)
     p = Plan.from_workload(wl, lanes=lanes)
+    if spw or interval:
+        p.set_layout(lanes, spw, interval)
     pi = torch.from_numpy(wl.pose).to(dev); tg = torch.from_numpy(wl.targets).to(dev); po = torch.empty_like(pi)
     st = torch.cuda.current_stream(dev).cuda_stream
     p.solve(pi.data_ptr(), tg.data_ptr(), po.data_ptr(), 0, n, st); torch.cuda.synchronize()
@@ -26,7 +30,7 @@ for case in sys.argv[1:]:
     v = list(buf)
     inf = p.info()
     waves = (n + inf['skeletons_per_block'] - 1) // inf['skeletons_per_block']
-    out = dict(cfg=cfg, n=n, lanes=inf['lanes_per_skeleton'], spw=inf['skeletons_per_block'],
+    out = dict(cfg=cfg, n=n, lanes=inf['lanes_per_skeleton'], spw=inf['skeletons_per_block'], case=case,
                cycles_per_wave=round(v[7] / waves))
     out.update({k: round(x / max(1, v[7]), 4) for k, x in zip(NAMES, v) if k != "total"})
     print(json.dumps(out), flush=True)
