@@ -1316,6 +1316,16 @@ int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const flo
 	DeviceGuard guard(p->device);
 	hipStream_t st = reinterpret_cast<hipStream_t>(hip_stream);
 	const int lanes = p->lanes_override;
+	{
+		// A launch whose skeletons are all resident at the default layout is bound by one
+		// skeleton's dependency chain; no layout shortens that, so there is nothing to time.
+		p->spw_override = 0;
+		p->interval_override = 0;
+		int rc0 = ensure_schedule(p, count);
+		if (rc0 != MBIK_OK) return rc0;
+		if ((int64_t)blocks_per_cu(p, p->host.lds_block_bytes) * p->host.spw * p->cu_count >= count && p->host.g_interval == 1)
+			return MBIK_OK;
+	}
 	// Candidate layouts: for each checkpoint interval, the largest skeletons-per-block at each
 	// distinct residency (blocks per CU).  Every layout computes the same bits; only the time
 	// differs.
