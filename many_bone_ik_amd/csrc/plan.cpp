@@ -9,6 +9,8 @@
 #include <cmath>
 #include <cstring>
 #include <functional>
+#include <thread>
+#include <vector>
 
 #include "gd_math.h"
 
@@ -435,10 +437,12 @@ std::string build_skeletons(HostPlan &p, int32_t n, const float *setup_pose, con
 			for (size_t k = kids[b].size(); k-- > 0;) stack.push_back(kids[b][k]);
 		}
 	}
-	// Constraint contributions per slot (all named constraints on that bone, in order).
+	// Per-skeleton setup, skeletons split across host threads (each writes only its own
+	// SoA column s, so the result does not depend on the split).
+	auto setup_range = [&](int s0, int s1) {
 	std::vector<X3> L(B), G(B);
 	std::vector<B3> Dm(B);
-	for (int s = 0; s < n; s++) {
+	for (int s = s0; s < s1; s++) {
 		const float *pose = setup_pose + (size_t)s * B * 10;
 		for (int b = 0; b < B; b++) L[b] = (p.bone_flags[b] & BF_IN_LIST) ? pose_to_xform(pose + 10 * b) : xid();
 		for (int b : topo) {
@@ -556,6 +560,19 @@ std::string build_skeletons(HostPlan &p, int32_t n, const float *setup_pose, con
 				putd(CD_PER_CONE * k + 1, c.trcos);
 			}
 		}
+	}
+	};
+	const int hw = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+	const int nthreads = (int)std::min<int64_t>(hw, std::max<int64_t>(1, (int64_t)n / 64));
+	if (nthreads <= 1) {
+		setup_range(0, n);
+	} else {
+		std::vector<std::thread> pool;
+		for (int t = 0; t < nthreads; t++) {
+			const int s0 = (int)((int64_t)n * t / nthreads), s1 = (int)((int64_t)n * (t + 1) / nthreads);
+			pool.emplace_back(setup_range, s0, s1);
+		}
+		for (auto &th : pool) th.join();
 	}
 	return "";
 }
