@@ -120,6 +120,19 @@ int32_t mbik_plan_set_launch(mbik_plan *plan, int32_t lanes_per_skeleton);
  * the parents of segment roots).  Results do not depend on the layout. */
 int32_t mbik_plan_set_layout(mbik_plan *plan, int32_t lanes_per_skeleton, int32_t skeletons_per_block,
 		int32_t global_checkpoint_interval);
+/* Re-derives the per-skeleton setup data (bone-direction frames, Kusudama cones, tangent
+ * circles and twist frames -- what mbik_plan_create computes on the host from the setup
+ * pose, ManyBoneIK3D::_bone_list_changed many_bone_ik_3d.cpp:1011-1068) on the GPU for
+ * skeletons [first, first+count), from device buffers indexed from skeleton `first`:
+ * setup_pose [count][bones][10], cones [count][constraints][max_cones][4], twist
+ * [count][constraints][2].  Same topology, pins and constraint bones as the plan; the
+ * result equals the host builder's.  Synchronizes hip_stream. */
+int32_t mbik_plan_rebuild_setup(mbik_plan *plan, int32_t first, int32_t count, const float *setup_pose,
+		const float *cones, const float *twist, void *hip_stream);
+/* Copies the plan's per-skeleton setup tables to host buffers (any may be NULL):
+ * D [bones][9][n], CF [slots][14 + 13*max_cones][n] floats, CD [slots][2*max_cones][n]
+ * doubles, n = skeleton_count; slots = constraints on bones in the IK bone list. */
+int32_t mbik_plan_setup_tables(const mbik_plan *plan, float *D, float *CF, double *CD);
 /* Diagnostic: how many one-wave blocks using lds_bytes_per_block of LDS one CU of the plan's
  * device holds at once (the runtime occupancy query for the plan's kernel). */
 int32_t mbik_plan_resident_blocks(const mbik_plan *plan, int64_t lds_bytes_per_block);

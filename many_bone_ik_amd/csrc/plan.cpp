@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "gd_math.h"
+#include "setup.h"
 
 namespace mbik {
 
@@ -303,264 +304,81 @@ std::string build_topology(const mbik_skeleton_desc &desc, const mbik_config &cf
 	return "";
 }
 
-// ---------------------------------------------------------------------------------------
-// IKLimitCone3D / IKRay3D setup geometry (ik_open_cone_3d.cpp:36-120, ik_ray_3d.cpp:64-166)
-// ---------------------------------------------------------------------------------------
-namespace {
-struct Cone {
-	V3 cp = {0, 1, 0};
-	double radius = 0, rcos = 0;
-	V3 t1 = {0, 0, 0}, t2 = {0, 0, 0};
-	double tr = 0, trcos = 0;
-};
-struct Ray {
-	V3 p1, p2;
-};
-void elongate(Ray &r, float amt) {
-	V3 mid = (r.p1 + r.p2) * 0.5f;
-	V3 h1 = r.p1 - mid, h2 = r.p2 - mid;
-	V3 a1 = normalized(h1) * amt, a2 = normalized(h2) * amt;
-	r.p1 = h1 + a1 + mid;
-	r.p2 = h2 + a2 + mid;
-}
-V3 intersects_plane(const Ray &r, V3 ta, V3 tb, V3 tc) {
-	V3 tta = ta - r.p1, ttb = tb - r.p1, ttc = tc - r.p1;
-	V3 u = ttb - tta, v = ttc - tta;
-	V3 dir = r.p2 - r.p1;
-	V3 n = normalized(cross(u, v));
-	V3 w0 = v3(0, 0, 0) - tta;
-	float a = -(dot(n, w0));
-	float b = dot(n, dir);
-	float rr = a / b;
-	return dir * rr + r.p1;
-}
-void intersects_sphere(const Ray &r, float radius, V3 &S1, V3 &S2) {
-	V3 rp1 = r.p1 - v3(0, 0, 0), rp2 = r.p2 - v3(0, 0, 0);
-	V3 e = normalized(rp2 - rp1);
-	V3 h = v3(0, 0, 0) - rp1;
-	float lf = dot(e, h);
-	float radpow = radius * radius;
-	float hdh = length_sq(h);
-	float lfpow = lf * lf;
-	float s = radpow - hdh + lfpow;
-	if (s >= 0.0f) {
-		s = sqrtf(s);
-		if (lf < s) {
-			if (lf + s >= 0) s = -s;
-		}
-		S1 = e * (lf - s) + rp1;
-		S2 = e * (lf + s) + rp1;
-	}
-	S1 = S1 + v3(0, 0, 0);
-	S2 = S2 + v3(0, 0, 0);
-}
-V3 get_orthogonal(V3 p) {
-	float threshold = length(p) * 0.6f;
-	if (threshold > 0.f) {
-		if (fabsf(p.x) <= threshold) {
-			float inv = 1.f / sqrtf(p.y * p.y + p.z * p.z);
-			return v3(0.f, inv * p.z, -inv * p.y);
-		} else if (fabsf(p.y) <= threshold) {
-			float inv = 1.f / sqrtf(p.x * p.x + p.z * p.z);
-			return v3(-inv * p.z, 0.f, inv * p.x);
-		}
-		float inv = 1.f / sqrtf(p.x * p.x + p.y * p.y);
-		return v3(inv * p.y, -inv * p.x, 0.f);
-	}
-	return v3(0, 0, 0);
-}
-void set_control_point(Cone &c, V3 v) {
-	if (is_zero_approx(length_sq(v))) c.cp = v3(0, 1, 0);
-	else c.cp = normalized(v);
-}
-void update_tangent_handles(Cone &c, const Cone *next) {
-	if (!next) return;
-	double radA = c.radius, radB = next->radius;
-	V3 A = c.cp, Bv = next->cp;
-	V3 arc_normal = normalized(cross(A, Bv));
-	double tRadius = (gd::PI - (radA + radB)) / 2;
-	double bA = radA + tRadius, bB = radB + tRadius;
-	V3 scaledAxisA = A * (float)std::cos(bA);
-	V3 planeDir1A = xform(axis_angle_sq(arc_normal, (float)bA), A);
-	V3 planeDir2A = xform(axis_angle_sq(A, (float)(gd::PI / 2)), planeDir1A);
-	V3 scaledAxisB = Bv * (float)std::cos(bB);
-	V3 planeDir1B = xform(axis_angle_sq(arc_normal, (float)bB), Bv);
-	V3 planeDir2B = xform(axis_angle_sq(Bv, (float)(gd::PI / 2)), planeDir1B);
-	Ray r1B{planeDir1B, scaledAxisB}, r2B{planeDir1B, planeDir2B};
-	elongate(r1B, 99);
-	elongate(r2B, 99);
-	V3 i1 = intersects_plane(r1B, scaledAxisA, planeDir1A, planeDir2A);
-	V3 i2 = intersects_plane(r2B, scaledAxisA, planeDir1A, planeDir2A);
-	Ray ir{i1, i2};
-	elongate(ir, 99);
-	V3 S1 = v3(0, 0, 0), S2 = v3(0, 0, 0);
-	intersects_sphere(ir, 1.0f, S1, S2);
-	c.t1 = normalized(S1);
-	c.t2 = normalized(S2);
-	c.tr = tRadius;
-	c.trcos = std::cos(tRadius);
-	if (is_zero_approx(length_sq(c.t1))) c.t1 = normalized(get_orthogonal(c.cp));
-	if (is_zero_approx(length_sq(c.t2))) c.t2 = normalized(get_orthogonal(c.t1 * -1.0f));
-}
-void update_tangent_radii(std::vector<Cone> &cs) {
-	for (size_t i = 0; i < cs.size(); i++) update_tangent_handles(cs[i], i + 1 < cs.size() ? &cs[i + 1] : nullptr);
-}
-} // namespace
 
 // ---------------------------------------------------------------------------------------
 // Per-skeleton setup data
 // ---------------------------------------------------------------------------------------
+void setup_tables(HostPlan &p) {
+	const int B = p.B;
+	std::vector<std::vector<int>> kids(B);
+	for (int b = 0; b < B; b++)
+		if (p.parents[b] >= 0) kids[p.parents[b]].push_back(b);
+	p.setup_topo.clear();
+	std::vector<int> stack;
+	for (int b = B; b-- > 0;)
+		if (p.parents[b] < 0) stack.push_back(b);
+	while (!stack.empty()) {
+		int b = stack.back();
+		stack.pop_back();
+		p.setup_topo.push_back(b);
+		for (size_t k = kids[b].size(); k-- > 0;) stack.push_back(kids[b][k]);
+	}
+	p.ik_child_off.assign(1, 0);
+	p.ik_children.clear();
+	for (int b = 0; b < B; b++) {
+		for (int c = 0; c < B; c++)
+			if (p.bone_ik_parent[c] == b) p.ik_children.push_back(c);
+		p.ik_child_off.push_back((int)p.ik_children.size());
+	}
+}
+
+SetupView setup_view(const HostPlan &p, int32_t n, int32_t max_cones_in) {
+	SetupView v;
+	v.B = p.B;
+	v.NC = p.NC;
+	v.N = n;
+	v.max_cones_in = max_cones_in;
+	v.desc_constraint_count = p.desc_constraint_count;
+	v.cfs = p.cf_stride();
+	v.cds = p.cd_stride();
+	v.n_topo = (int)p.setup_topo.size();
+	v.n_list = (int)p.bone_list.size();
+	v.n_cons_order = (int)p.cons_order.size();
+	v.topo = p.setup_topo.data();
+	v.bone_list = p.bone_list.data();
+	v.bone_flags = p.bone_flags.data();
+	v.bone_pose_parent = p.bone_pose_parent.data();
+	v.bone_ik_parent = p.bone_ik_parent.data();
+	v.ik_child_off = p.ik_child_off.data();
+	v.ik_children = p.ik_children.data();
+	v.cons_order = p.cons_order.data();
+	v.cons_order_slot = p.cons_order_slot.data();
+	v.cons_order_ncones = p.cons_order_ncones.data();
+	v.cons_bone = p.cons_bone.data();
+	return v;
+}
+
 std::string build_skeletons(HostPlan &p, int32_t n, const float *setup_pose, const float *cones, const float *twist,
 		int32_t max_cones_in) {
 	const int B = p.B, NC = p.NC;
 	if (n <= 0 || !setup_pose) return "n_skeletons must be > 0 and setup_pose non-null";
 	if (NC > 0 && (!cones || !twist)) return "cones/twist required when constraints exist";
+	for (int c : p.cons_order_ncones)
+		if (c > max_cones_in) return "a constraint has more cones than max_cones";
 	p.N = n;
 	const size_t N = (size_t)n;
 	p.D.assign((size_t)B * 9 * N, 0.0f);
-	const int cfs = p.cf_stride(), cds = p.cd_stride();
-	p.CF.assign((size_t)NC * cfs * N, 0.0f);
-	p.CD.assign((size_t)NC * cds * N, 0.0);
-	// topological order (parents first)
-	std::vector<int> topo;
-	{
-		std::vector<std::vector<int>> kids(B);
-		for (int b = 0; b < B; b++)
-			if (p.parents[b] >= 0) kids[p.parents[b]].push_back(b);
-		std::vector<int> stack;
-		for (int b = B; b-- > 0;)
-			if (p.parents[b] < 0) stack.push_back(b);
-		while (!stack.empty()) {
-			int b = stack.back();
-			stack.pop_back();
-			topo.push_back(b);
-			for (size_t k = kids[b].size(); k-- > 0;) stack.push_back(kids[b][k]);
-		}
-	}
-	// Per-skeleton setup, skeletons split across host threads (each writes only its own
-	// SoA column s, so the result does not depend on the split).
+	p.CF.assign((size_t)NC * p.cf_stride() * N, 0.0f);
+	p.CD.assign((size_t)NC * p.cd_stride() * N, 0.0);
+	setup_tables(p);
+	p.setup_max_cones = std::max(1, max_cones_in);
+	const SetupView v = setup_view(p, n, max_cones_in);
+	// Skeletons split across host threads; each writes only its own SoA column s.
 	auto setup_range = [&](int s0, int s1) {
-	std::vector<X3> L(B), G(B);
-	std::vector<B3> Dm(B);
-	for (int s = s0; s < s1; s++) {
-		const float *pose = setup_pose + (size_t)s * B * 10;
-		for (int b = 0; b < B; b++) L[b] = (p.bone_flags[b] & BF_IN_LIST) ? pose_to_xform(pose + 10 * b) : xid();
-		for (int b : topo) {
-			int pp = p.bone_pose_parent[b];
-			if (pp >= 0) G[b] = G[pp] * L[b];
-			else if (pp == POSE_PARENT_ORIGIN) G[b] = xid() * L[b];
-			else G[b] = L[b];
-		}
-		for (int b = 0; b < B; b++) Dm[b] = bid();
-		// IKBone3D::update_default_bone_direction_transform (ik_bone_3d.cpp:57-93), bone_list order.
-		for (int b : p.bone_list) {
-			V3 cc = v3(0, 0, 0);
-			int count = 0;
-			for (int c = 0; c < B; c++)
-				if (p.bone_ik_parent[c] == b) {
-					cc = cc + G[c].o;
-					count++;
-				}
-			cc = divs(cc, (float)count); // count == 0 -> 0/0 (NaN), as the reference
-			cc = cc - G[b].o;
-			if (is_zero_approx(length_sq(cc))) {
-				int par = p.bone_ik_parent[b];
-				cc = par >= 0 ? col(G[par].b * Dm[par], 1) : col(G[b].b * Dm[b], 1);
-			}
-			if (!is_zero_approx(length_sq(cc)) && count > 0) {
-				cc = normalized(cc);
-				V3 bd = normalized(col(G[b].b * Dm[b], 1));
-				B3 P = G[b].b;
-				Dm[b] = ((inverse(P) * from_quat(arc(cc, bd))) * P) * Dm[b];
-			}
-		}
-		for (int b = 0; b < B; b++)
-			for (int f = 0; f < 9; f++) p.D[((size_t)b * 9 + f) * N + s] = Dm[b].r[f / 3][f % 3];
-		if (NC == 0) continue;
-		// Kusudama setup, in the constraint order of the description (:1037-1067).
-		std::vector<B3> T(NC, bid());
-		std::vector<std::vector<Cone>> kc(NC);
-		std::vector<Q> tcr(NC, qid());
-		std::vector<float> thc(NC, 0.0f);
-		for (int c = 0; c < (int)p.cons_order.size(); c++) {
-			int ci = p.cons_order[c];        // index into the description's constraint array
-			int slot = p.cons_order_slot[c];
-			int b = p.cons_bone[slot];
-			int ncones = p.cons_order_ncones[c];
-			const float *cn = cones + ((size_t)s * p.desc_constraint_count + ci) * max_cones_in * 4;
-			const float *tw = twist + ((size_t)s * p.desc_constraint_count + ci) * 2;
-			std::vector<Cone> cs;
-			for (int k = 0; k < ncones; k++) {
-				Cone cone;
-				double rad = cn[4 * k + 3];
-				cone.radius = 1.0e-38 > rad ? 1.0e-38 : rad;
-				cone.rcos = std::cos(cone.radius);
-				set_control_point(cone, normalized(v3(cn[4 * k], cn[4 * k + 1], cn[4 * k + 2])));
-				cs.push_back(cone);
-				update_tangent_radii(cs);
-			}
-			// set_axial_limits (ik_kusudama_3d.cpp:103-115)
-			float min_angle = tw[0], range = tw[1];
-			V3 y_axis = v3(0, 1, 0), z_axis = v3(0, 0, 1);
-			Q twist_min_rot = axis_angle_sq(y_axis, min_angle);
-			V3 twist_min_vec = normalized(xform(twist_min_rot, z_axis));
-			V3 twist_center_vec = normalized(xform(twist_min_rot, twist_min_vec));
-			tcr[slot] = arc(z_axis, twist_center_vec);
-			thc[slot] = cos_f(range / 4.0f);
-			// _update_constraint(twist node) (ik_kusudama_3d.cpp:37-89)
-			V3 sum = v3(0, 0, 0);
-			int nd = 0;
-			if (cs.size() == 1) {
-				sum = sum + cs[0].cp;
-				nd = 1;
-			} else {
-				for (int k = 0; k + 1 < (int)cs.size(); k++) {
-					Q ttn = arc(cs[k].cp, cs[k + 1].cp);
-					V3 axis = get_axis(ttn);
-					double angle = get_angle(ttn) / 2.0;
-					V3 half = xform(axis_angle_basis(axis, (float)angle), cs[k].cp);
-					half = half * get_angle(ttn);
-					half = normalized(half);
-					sum = sum + half;
-					nd++;
-				}
-			}
-			V3 new_y = sum;
-			if (nd) new_y = normalized(divs(new_y, (float)nd));
-			int par = p.bone_ik_parent[b];
-			if (par >= 0) {
-				B3 gb = G[par].b * T[slot]; // twist node global = parent pose global * local
-				Q otn = arc(normalized(col(gb, 1)), normalized(xform(gb, new_y)));
-				B3 Pb = G[par].b;
-				T[slot] = ((inverse(Pb) * from_quat(otn)) * Pb) * T[slot];
-			}
-			for (auto &cone : cs) set_control_point(cone, normalized(cone.cp));
-			update_tangent_radii(cs);
-			kc[slot] = cs;
-		}
-		for (int slot = 0; slot < NC; slot++) {
-			auto put = [&](int f, float v) { p.CF[((size_t)slot * cfs + f) * N + s] = v; };
-			auto putd = [&](int f, double v) { p.CD[((size_t)slot * cds + f) * N + s] = v; };
-			put(CF_TWIST_Q + 0, tcr[slot].x);
-			put(CF_TWIST_Q + 1, tcr[slot].y);
-			put(CF_TWIST_Q + 2, tcr[slot].z);
-			put(CF_TWIST_Q + 3, tcr[slot].w);
-			put(CF_TWIST_COS, thc[slot]);
-			for (int f = 0; f < 9; f++) put(CF_TWIST_T + f, T[slot].r[f / 3][f % 3]);
-			for (int k = 0; k < (int)kc[slot].size(); k++) {
-				const Cone &c = kc[slot][k];
-				int o = CF_CONE0 + CF_PER_CONE * k;
-				float rf = (float)c.radius, trf = (float)c.tr;
-				put(o + CFC_CP + 0, c.cp.x); put(o + CFC_CP + 1, c.cp.y); put(o + CFC_CP + 2, c.cp.z);
-				put(o + CFC_SR, sin_f(rf * 0.5f)); put(o + CFC_CR, cos_f(rf * 0.5f));
-				put(o + CFC_T1 + 0, c.t1.x); put(o + CFC_T1 + 1, c.t1.y); put(o + CFC_T1 + 2, c.t1.z);
-				put(o + CFC_T2 + 0, c.t2.x); put(o + CFC_T2 + 1, c.t2.y); put(o + CFC_T2 + 2, c.t2.z);
-				put(o + CFC_ST, sin_f(trf * 0.5f)); put(o + CFC_CT, cos_f(trf * 0.5f));
-				putd(CD_PER_CONE * k + 0, c.rcos);
-				putd(CD_PER_CONE * k + 1, c.trcos);
-			}
-		}
-	}
+		std::vector<char> buf(setup_scratch_bytes(B, NC, std::max(1, max_cones_in)));
+		const SetupScratch w = setup_scratch_at(buf.data(), B, NC, std::max(1, max_cones_in));
+		for (int s = s0; s < s1; s++)
+			setup_skeleton(v, s, s, setup_pose + (size_t)s * B * 10, cones, twist, w, p.D.data(), p.CF.data(), p.CD.data());
 	};
 	const int hw = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
 	const int nthreads = (int)std::min<int64_t>(hw, std::max<int64_t>(1, (int64_t)n / 64));

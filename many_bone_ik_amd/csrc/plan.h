@@ -75,6 +75,9 @@ struct HostPlan {
 	std::vector<int32_t> cons_bone, cons_ncones;    // constraint slots (bones in the list only)
 	std::vector<int32_t> cons_order, cons_order_slot, cons_order_ncones; // applied constraints, desc order
 	int32_t desc_constraint_count = 0;
+	std::vector<int32_t> setup_topo;                // bones, parents before children
+	std::vector<int32_t> ik_child_off, ik_children; // IK children of each bone, ascending (setup.h)
+	int32_t setup_max_cones = 1;                    // cones stride of the setup inputs
 	int32_t max_headings = 0;
 	// ---- launch shape ----
 	int32_t K = 4, log2K = 2, spw = 16;
@@ -102,6 +105,10 @@ std::string build_topology(const mbik_skeleton_desc &desc, const mbik_config &cf
 // Fills D / CF / CD for skeletons [0, n) from their setup poses, cones and twist.
 std::string build_skeletons(HostPlan &plan, int32_t n, const float *setup_pose, const float *cones, const float *twist,
 		int32_t max_cones_in);
+// Host-side tables the per-skeleton setup reads (setup.h); filled by build_skeletons.
+void setup_tables(HostPlan &plan);
+struct SetupView;
+SetupView setup_view(const HostPlan &plan, int32_t n, int32_t max_cones_in);
 // Chooses lanes-per-skeleton / skeletons-per-block and the sibling-level schedule.
 // spw_override / interval_override: 0 = automatic (mbik_plan_set_layout).
 // blocks_per_cu(lds_bytes): how many one-wave blocks of that LDS size a CU holds at once

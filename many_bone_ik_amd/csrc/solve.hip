@@ -33,6 +33,7 @@
 
 #include "gd_math.h"
 #include "plan.h"
+#include "setup.h"
 
 using namespace gd;
 
@@ -998,6 +999,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MBIK_WAVES_P
 // ======================================================================================
 // Host side: plan upload, launches, C ABI
 // ======================================================================================
+// GPU plan setup: the per-skeleton bone-direction and Kusudama frames of
+// mbik_plan_create, derived on the device with the host builder's own code (setup.h), one
+// thread per skeleton over a grid-stride loop, each with a private scratch slice.
+__global__ __launch_bounds__(64) void mbik_setup_kernel(mbik::SetupView v, int first, int count, const float *__restrict__ pose,
+		const float *__restrict__ cones, const float *__restrict__ twist, char *scratch, size_t scratch_stride, float *D,
+		float *CF, double *CD) {
+	const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+	const int nthreads = gridDim.x * blockDim.x;
+	const mbik::SetupScratch w = mbik::setup_scratch_at(scratch + (size_t)tid * scratch_stride, v.B, v.NC, v.max_cones_in);
+	for (int i = tid; i < count; i += nthreads)
+		mbik::setup_skeleton(v, i, first + i, pose + (size_t)i * v.B * 10, cones, twist, w, D, CF, CD);
+}
+
 struct mbik_plan {
 	mbik::HostPlan host;
 	int device = 0;
@@ -1013,6 +1027,9 @@ struct mbik_plan {
 	// scratch for mbik_solve_host
 	float *d_in = nullptr, *d_tg = nullptr, *d_out = nullptr;
 	size_t scratch_skel = 0;
+	// device copies of the setup tables (mbik_plan_rebuild_setup)
+	mbik::SetupView dsetup{};
+	bool dsetup_ready = false;
 };
 
 namespace {
@@ -1300,6 +1317,67 @@ int32_t mbik_plan_set_layout(mbik_plan *p, int32_t lanes, int32_t skeletons_per_
 	p->spw_override = skeletons_per_block;
 	p->interval_override = global_checkpoint_interval;
 	p->sched_K = -1;
+	return MBIK_OK;
+}
+
+int32_t mbik_plan_rebuild_setup(mbik_plan *p, int32_t first, int32_t count, const float *setup_pose, const float *cones,
+		const float *twist, void *hip_stream) {
+	if (!p) return fail(MBIK_EINVAL, "null plan");
+	mbik::HostPlan &h = p->host;
+	if (first < 0 || count < 0 || (int64_t)first + count > h.N) return fail(MBIK_EINVAL, "skeleton range out of plan");
+	if (count == 0) return MBIK_OK;
+	if (!setup_pose || (h.NC > 0 && (!cones || !twist))) return fail(MBIK_EINVAL, "null buffer");
+	DeviceGuard guard(p->device);
+	if (!p->dsetup_ready) {
+		mbik::SetupView v = mbik::setup_view(h, h.N, h.setup_max_cones);
+		int rc = 0;
+		auto up = [&](const std::vector<int32_t> &vec, const int *&dst) {
+			if (rc == 0) rc = upload(p, vec, dst);
+		};
+		up(h.setup_topo, v.topo);
+		up(h.bone_list, v.bone_list);
+		up(h.bone_flags, v.bone_flags);
+		up(h.bone_pose_parent, v.bone_pose_parent);
+		up(h.bone_ik_parent, v.bone_ik_parent);
+		up(h.ik_child_off, v.ik_child_off);
+		up(h.ik_children, v.ik_children);
+		up(h.cons_order, v.cons_order);
+		up(h.cons_order_slot, v.cons_order_slot);
+		up(h.cons_order_ncones, v.cons_order_ncones);
+		up(h.cons_bone, v.cons_bone);
+		if (rc) return rc;
+		p->dsetup = v;
+		p->dsetup_ready = true;
+	}
+	const mbik::SetupView &v = p->dsetup;
+	const size_t stride = (mbik::setup_scratch_bytes(v.B, v.NC, v.max_cones_in) + 255) & ~size_t(255);
+	const int threads = std::min(count, 8192);
+	void *scratch = nullptr;
+	if (hipMalloc(&scratch, stride * (size_t)threads) != hipSuccess) return fail(MBIK_ENOMEM, "hipMalloc setup scratch");
+	hipStream_t st = reinterpret_cast<hipStream_t>(hip_stream);
+	const DevPlan &d = p->dev;
+	hipLaunchKernelGGL(mbik_setup_kernel, dim3((threads + 63) / 64), dim3(64), 0, st, v, first, count, setup_pose, cones, twist,
+			static_cast<char *>(scratch), stride, const_cast<float *>(d.D), const_cast<float *>(d.CF),
+			const_cast<double *>(d.CD));
+	hipError_t e = hipGetLastError();
+	// the scratch is freed after the kernel: hipFree synchronizes the device
+	(void)hipStreamSynchronize(st);
+	(void)hipFree(scratch);
+	if (e != hipSuccess) return fail(MBIK_EHIP, std::string("setup launch: ") + hipGetErrorString(e));
+	return MBIK_OK;
+}
+
+int32_t mbik_plan_setup_tables(const mbik_plan *p, float *D, float *CF, double *CD) {
+	if (!p) return fail(MBIK_EINVAL, "null plan");
+	const mbik::HostPlan &h = p->host;
+	DeviceGuard guard(p->device);
+	const size_t N = (size_t)h.N;
+	if (D && hipMemcpy(D, p->dev.D, (size_t)h.B * 9 * N * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess)
+		return fail(MBIK_EHIP, "hipMemcpy D");
+	if (CF && h.NC && hipMemcpy(CF, p->dev.CF, (size_t)h.NC * h.cf_stride() * N * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess)
+		return fail(MBIK_EHIP, "hipMemcpy CF");
+	if (CD && h.NC && hipMemcpy(CD, p->dev.CD, (size_t)h.NC * h.cd_stride() * N * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess)
+		return fail(MBIK_EHIP, "hipMemcpy CD");
 	return MBIK_OK;
 }
 

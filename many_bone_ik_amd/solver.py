@@ -62,7 +62,9 @@ def describe_topology(parents, pins, constraints=(), *, iterations=15, default_d
                       bone_damp=None) -> dict:
     """Host-only segmentation (mbik_describe_topology): bone_list + post-order segment table."""
     L = _lib.load()
-    d = _Desc(parents, pins, list(constraints), 1, iterations, default_damp, False, 0, bone_damp)
+    constraints = list(constraints)
+    mc = max([1] + [int(c.get("cone_count", 0)) for c in constraints])
+    d = _Desc(parents, pins, constraints, mc, iterations, default_damp, False, 0, bone_damp)
     B = d.parents.shape[0]
     bl = np.zeros(B, np.int32); nbl = C.c_int32(0)
     r = np.zeros(B, np.int32); t = np.zeros(B, np.int32); p = np.zeros(B, np.int32); nh = np.zeros(B, np.int32)
@@ -93,6 +95,12 @@ class Plan:
         self.h = h
         self.n = n
         self.B = B
+        # constraint slots = constraints whose bone is in the IK bone list (plan.cpp)
+        bl = set(describe_topology(parents, pins, constraints, iterations=iterations, default_damp=default_damp,
+                                   bone_damp=bone_damp)["bone_list"].tolist())
+        self._slots = len({int(c["bone"]) for c in constraints if int(c["bone"]) in bl})
+        self._cf_stride = 14 + 13 * max(1, int(mc))
+        self._cd_stride = 2 * max(1, int(mc))
         self.P = len(pins)
         self.iterations = int(iterations)
         if lanes:
@@ -126,6 +134,25 @@ class Plan:
         count = self.n - first if count is None else count
         check(self._L.mbik_plan_autotune(self.h, first, count, C.c_void_p(pose_in_ptr), C.c_void_p(targets_ptr),
                                          C.c_void_p(pose_out_ptr), C.c_void_p(stream or None)))
+
+    def rebuild_setup(self, setup_pose_ptr: int, cones_ptr: int = 0, twist_ptr: int = 0, first: int = 0,
+                      count: int | None = None, stream: int = 0):
+        """mbik_plan_rebuild_setup: re-derive the per-skeleton setup data on the GPU."""
+        count = self.n - first if count is None else count
+        check(self._L.mbik_plan_rebuild_setup(self.h, first, count, C.c_void_p(setup_pose_ptr),
+                                              C.c_void_p(cones_ptr or None), C.c_void_p(twist_ptr or None),
+                                              C.c_void_p(stream or None)))
+
+    def setup_tables(self):
+        """(D, CF, CD) per-skeleton setup tables as numpy arrays (mbik_plan_setup_tables)."""
+        inf = self.info()
+        n, B = inf["skeleton_count"], inf["bone_count"]
+        D = np.zeros((B, 9, n), np.float32)
+        slots, cfs, cds = self._slots, self._cf_stride, self._cd_stride
+        CF = np.zeros((slots, cfs, n), np.float32)
+        CD = np.zeros((slots, cds, n), np.float64)
+        check(self._L.mbik_plan_setup_tables(self.h, _ptr(D), _ptr(CF) if slots else None, _ptr(CD) if slots else None))
+        return D, CF, CD
 
     def solve(self, pose_in_ptr: int, targets_ptr: int, pose_out_ptr: int, first: int = 0, count: int | None = None,
               stream: int = 0):
