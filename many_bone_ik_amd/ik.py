@@ -54,7 +54,7 @@ class ManyBoneIK3D:
     def set_total_effector_count(self, count: int):       # many_bone_ik_3d.cpp:44-52
         while len(self._pins) < count:
             self._pins.append(dict(name="", weight=0.0, direction_priorities=(0.2, 0.0, 0.2),
-                                   motion_propagation_factor=1.0))
+                                   motion_propagation_factor=1.0, target_node=""))
         del self._pins[count:]
         self.set_dirty()
 
@@ -93,6 +93,13 @@ class ManyBoneIK3D:
     def get_pin_motion_propagation_factor(self, i: int) -> float:
         return self._pins[i]["motion_propagation_factor"] if 0 <= i < len(self._pins) else 0.0
 
+    def set_effector_target_node_path(self, i: int, path: str):   # many_bone_ik_3d.cpp:62-72
+        if 0 <= i < len(self._pins):
+            self._pins[i]["target_node"] = str(path)
+
+    def get_effector_target_node_path(self, i: int) -> str:
+        return self._pins[i]["target_node"] if 0 <= i < len(self._pins) else ""
+
     # ----------------------------------------------------------------- constraints
     def _set_constraint_count(self, count: int):           # many_bone_ik_3d.cpp:455-471
         while len(self._constraints) < count:
@@ -126,18 +133,32 @@ class ManyBoneIK3D:
     def get_kusudama_open_cone_count(self, i: int) -> int:
         return self._constraints[i]["cone_count"] if 0 <= i < len(self._constraints) else 0
 
-    def set_kusudama_open_cone(self, i: int, j: int, center, radius: float):   # :545-563
+    def set_kusudama_open_cone_center(self, i: int, j: int, center):   # :578-592 (stored as given)
         if not 0 <= i < len(self._constraints):
             return
         cones = self._constraints[i]["cones"]
         if not 0 <= j < len(cones):
             return
-        c = np.asarray(center, np.float32)
-        if abs(float(np.dot(c, c))) < 1e-5:
-            c = np.array([0.0, 1.0, 0.0], np.float32)
-        c = c / np.linalg.norm(c)
-        cones[j] = (float(c[0]), float(c[1]), float(c[2]), float(radius))
+        c = [float(x) for x in np.asarray(center, np.float32)]
+        if abs(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]) < 1e-5:   # Math::is_zero_approx(length_squared)
+            c = [0.0, 1.0, 0.0]
+        cones[j] = (c[0], c[1], c[2], cones[j][3])
         self.set_dirty()
+
+    def set_kusudama_open_cone_radius(self, i: int, j: int, radius: float):   # :568-576
+        if not 0 <= i < len(self._constraints):
+            return
+        c = self._constraints[i]
+        if not (0 <= j < c["cone_count"] and j < len(c["cones"])):
+            return
+        cx, cy, cz, _ = c["cones"][j]
+        c["cones"][j] = (cx, cy, cz, float(radius))
+        self.set_dirty()
+
+    def set_kusudama_open_cone(self, i: int, j: int, center, radius: float):
+        """Convenience: set_kusudama_open_cone_center + set_kusudama_open_cone_radius."""
+        self.set_kusudama_open_cone_center(i, j, center)
+        self.set_kusudama_open_cone_radius(i, j, radius)
 
     def get_kusudama_open_cone_center(self, i: int, j: int):
         try:
@@ -151,7 +172,7 @@ class ManyBoneIK3D:
         except IndexError:
             return math.tau
 
-    def set_joint_twist(self, i: int, twist):
+    def set_joint_twist(self, i: int, twist):                      # :488-492
         if 0 <= i < len(self._constraints):
             self._constraints[i]["twist"] = (float(twist[0]), float(twist[1]))
             self.set_dirty()

@@ -104,3 +104,25 @@ def test_host_api_mirror_end_to_end(oracle, mbik):
     got = ik.process_modification(wl.pose, wl.targets, cones=wl.cones, twist=wl.twist)
     ref = oracle.Oracle(wl).solve(wl.pose, wl.targets)
     assert_parity(got, ref, "ManyBoneIK3D mirror")
+
+
+def test_rig_loaded_from_scene_properties(oracle, mbik):
+    """A rig configured from Godot scene properties (many_bone_ik_amd.config), solved on the
+    GPU through the ManyBoneIK3D mirror, vs the oracle given the same configuration."""
+    from many_bone_ik_amd import config as cfgmod
+    from tests.test_config import BONES, PARENTS, SCENE
+    ik = cfgmod.load_tscn(SCENE, PARENTS, BONES, godot_twist_roundtrip=True)
+    n = 16
+    topo = W.custom_topology(PARENTS, [4, 6], [3, 5], cones_per_bone=2, twist=(0.0, 1.0),
+                             iterations=ik.get_iterations_per_frame())
+    wl = W.generate(7, n, topo=topo)
+    cons, cones, twist, _ = ik._constraint_arrays(n)
+    wl.cones, wl.twist = cones, twist
+    wl.cone_count = np.array([c["cone_count"] for c in cons], np.int32)
+    wl.pin_weight = np.array([ik.get_pin_weight(i) for i in range(2)], np.float32)
+    wl.pin_priority = np.array([ik.get_pin_direction_priorities(i) for i in range(2)], np.float32)
+    wl.pin_propagation = np.array([ik.get_pin_motion_propagation_factor(i) for i in range(2)], np.float32)
+    ref = oracle.Oracle(wl, stabilization_passes=ik.get_stabilization_passes(),
+                        default_damp=ik.get_default_damp()).solve(wl.pose, wl.targets)
+    got = ik.process_modification(wl.pose, wl.targets)
+    assert_parity(got, ref, "scene-configured rig")

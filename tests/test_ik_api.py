@@ -34,14 +34,20 @@ def test_out_of_range_is_ignored_like_err_fail_index():
     assert ik.get_kusudama_open_cone_radius(0, 0) == math.tau
 
 
-def test_cone_center_normalised_and_zero_replaced():
+def test_cone_center_stored_as_given_and_zero_replaced():
+    """set_kusudama_open_cone_center stores the vector as given (the cone setup normalizes
+    it later, ik_open_cone_3d.cpp); a zero vector becomes +Y (many_bone_ik_3d.cpp:578-592)."""
     ik = make()
     ik._set_constraint_count(1)
     ik.set_kusudama_open_cone_count(0, 2)
+    assert ik.get_kusudama_open_cone_center(0, 1) == (0.0, -1.0, 0.0)   # new cone: -Y of an identity frame
+    assert ik.get_kusudama_open_cone_radius(0, 1) == 0.0
     ik.set_kusudama_open_cone(0, 0, (0, 0, 0), 0.3)
     ik.set_kusudama_open_cone(0, 1, (2, 0, 0), 0.2)
     assert ik.get_kusudama_open_cone_center(0, 0) == (0.0, 1.0, 0.0)
-    assert np.allclose(ik.get_kusudama_open_cone_center(0, 1), (1, 0, 0))
+    assert ik.get_kusudama_open_cone_center(0, 1) == (2.0, 0.0, 0.0)
+    ik.set_kusudama_open_cone_radius(0, 5, 1.0)  # out of range: ignored
+    assert ik.get_kusudama_open_cone_radius(0, 1) == 0.2
 
 
 def test_describe_segments(mbik):
