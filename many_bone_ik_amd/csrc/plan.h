@@ -37,8 +37,14 @@ constexpr int CF_TWIST_Q = 0;
 constexpr int CF_TWIST_COS = 4;
 constexpr int CF_TWIST_T = 5;
 constexpr int CF_CONE0 = 14;
-constexpr int CF_PER_CONE = 13;
+constexpr int CF_PER_CONE = 31;
 constexpr int CFC_CP = 0, CFC_SR = 3, CFC_CR = 4, CFC_T1 = 5, CFC_T2 = 8, CFC_ST = 11, CFC_CT = 12;
+// Per-cone constants the cone queries would otherwise re-derive every bone-step, computed at
+// setup with the same operations (so bitwise what the queries compute): the normalized
+// control point (closest_to_cone, ik_open_cone_3d.cpp:358-381) and, for the pair (cone,
+// next cone), cross(cp, next cp) and the four normalized edge normals of the tangent
+// triangles (get_on_great_tangent_triangle, :285-321).
+constexpr int CFC_NCP = 13, CFC_C1XC2 = 16, CFC_A1 = 19, CFC_A2 = 22, CFC_B1 = 25, CFC_B2 = 28;
 // Per-skeleton double fields of one constraint slot, per cone: radius cosine, tangent radius cosine.
 constexpr int CD_PER_CONE = 2;
 

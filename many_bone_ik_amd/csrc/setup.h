@@ -292,6 +292,18 @@ GDI void setup_skeleton(const SetupView &v, int s_in, int s, const float *pose, 
 			cf[(o + 5) * N] = c.t1.x; cf[(o + 6) * N] = c.t1.y; cf[(o + 7) * N] = c.t1.z;
 			cf[(o + 8) * N] = c.t2.x; cf[(o + 9) * N] = c.t2.y; cf[(o + 10) * N] = c.t2.z;
 			cf[(o + 11) * N] = sin_f(trf * 0.5f); cf[(o + 12) * N] = cos_f(trf * 0.5f);
+			const V3 ncp = normalized(c.cp);
+			cf[(o + CFC_NCP) * N] = ncp.x; cf[(o + CFC_NCP + 1) * N] = ncp.y; cf[(o + CFC_NCP + 2) * N] = ncp.z;
+			if (k + 1 < w.kcn[slot]) {
+				const V3 nx = w.kc[(size_t)slot * mc + k + 1].cp;
+				const V3 pr[5] = {cross(c.cp, nx), normalized(cross(c.cp, c.t1)), normalized(cross(c.t2, c.cp)),
+						normalized(cross(c.t1, nx)), normalized(cross(nx, c.t2))};
+				for (int q = 0; q < 5; q++) {
+					cf[(o + CFC_C1XC2 + 3 * q) * N] = pr[q].x;
+					cf[(o + CFC_C1XC2 + 3 * q + 1) * N] = pr[q].y;
+					cf[(o + CFC_C1XC2 + 3 * q + 2) * N] = pr[q].z;
+				}
+			}
 			cd[(CD_PER_CONE * k + 0) * N] = c.rcos;
 			cd[(CD_PER_CONE * k + 1) * N] = c.trcos;
 		}

@@ -312,9 +312,9 @@ __device__ __forceinline__ void effector_headings(const DevPlan &t, int e, int b
 }
 
 // IKLimitCone3D::closest_to_cone (ik_open_cone_3d.cpp:358-381)
-__device__ __forceinline__ V3 closest_to_cone(V3 cp, float sin_half_r, float cos_half_r, double rcos, V3 input, double &in_bounds) {
-	V3 ni = normalized(input);
-	V3 ncp = normalized(cp);
+// ni = input.normalized() and ncp = control_point.normalized() come in precomputed (the
+// point is the same for every cone; the control point is a per-skeleton constant).
+__device__ __forceinline__ V3 closest_to_cone(V3 ncp, float sin_half_r, float cos_half_r, double rcos, V3 ni, double &in_bounds) {
 	if ((double)dot(ni, ncp) > rcos) {
 		in_bounds = 1.0;
 		return v3(NAN, NAN, NAN);
@@ -328,12 +328,14 @@ __device__ __forceinline__ V3 closest_to_cone(V3 cp, float sin_half_r, float cos
 	return xform(rot_to, acp);
 }
 // IKLimitCone3D::get_on_great_tangent_triangle (ik_open_cone_3d.cpp:285-321)
-__device__ __forceinline__ V3 great_tangent_triangle(V3 cp, V3 ncp, V3 t1, V3 t2, float sin_half_tr, float cos_half_tr, double trcos, V3 input) {
-	V3 c1xc2 = cross(cp, ncp);
+// c1xc2 = cross(cp, next cp) and the normalized edge normals a1 = n(cp x t1), a2 = n(t2 x cp),
+// b1 = n(t1 x next cp), b2 = n(next cp x t2) are per-skeleton constants from the setup.
+__device__ __forceinline__ V3 great_tangent_triangle(V3 c1xc2, V3 a1, V3 a2, V3 b1, V3 b2, V3 t1, V3 t2, float sin_half_tr,
+		float cos_half_tr, double trcos, V3 input) {
 	double c1c2dir = dot(input, c1xc2);
 	V3 tc = c1c2dir < 0.0 ? t1 : t2;
-	V3 a = c1c2dir < 0.0 ? normalized(cross(cp, t1)) : normalized(cross(t2, cp));
-	V3 bb = c1c2dir < 0.0 ? normalized(cross(t1, ncp)) : normalized(cross(ncp, t2));
+	V3 a = c1c2dir < 0.0 ? a1 : a2;
+	V3 bb = c1c2dir < 0.0 ? b1 : b2;
 	if (dot(input, a) > 0 && dot(input, bb) > 0) {
 		if ((double)dot(input, tc) > trcos) {
 			V3 pn = normalized(cross(tc, input));
@@ -352,12 +354,13 @@ __device__ V3 local_point_in_limits(const DevPlan &t, int slot, size_t s, V3 in_
 	float closest_cos = -2.0f;
 	in_bounds = -1;
 	V3 closest = in_point;
+	const V3 npoint = normalized(point); // closest_to_cone's input.normalized(), the same for every cone
 	for (int i = 0; i < nc; i++) {
 		const int o = mbik::CF_CONE0 + mbik::CF_PER_CONE * i;
 		auto f = [&](int k) { return soa(t.CF, slot, t.cf_stride, o + k, t.N, s); };
-		V3 cp = v3(f(mbik::CFC_CP), f(mbik::CFC_CP + 1), f(mbik::CFC_CP + 2));
+		V3 ncp = v3(f(mbik::CFC_NCP), f(mbik::CFC_NCP + 1), f(mbik::CFC_NCP + 2));
 		double rcos = soad(t.CD, slot, t.cd_stride, mbik::CD_PER_CONE * i, t.N, s);
-		V3 c = closest_to_cone(cp, f(mbik::CFC_SR), f(mbik::CFC_CR), rcos, point, in_bounds);
+		V3 c = closest_to_cone(ncp, f(mbik::CFC_SR), f(mbik::CFC_CR), rcos, npoint, in_bounds);
 		if (is_nan3(c)) {
 			in_bounds = 1;
 			return point;
@@ -371,14 +374,11 @@ __device__ V3 local_point_in_limits(const DevPlan &t, int slot, size_t s, V3 in_
 	if (in_bounds == -1) {
 		for (int i = 0; i + 1 < nc; i++) {
 			const int o = mbik::CF_CONE0 + mbik::CF_PER_CONE * i;
-			const int on = o + mbik::CF_PER_CONE;
 			auto f = [&](int k) { return soa(t.CF, slot, t.cf_stride, k, t.N, s); };
-			V3 cp = v3(f(o + mbik::CFC_CP), f(o + mbik::CFC_CP + 1), f(o + mbik::CFC_CP + 2));
-			V3 ncp = v3(f(on + mbik::CFC_CP), f(on + mbik::CFC_CP + 1), f(on + mbik::CFC_CP + 2));
-			V3 t1 = v3(f(o + mbik::CFC_T1), f(o + mbik::CFC_T1 + 1), f(o + mbik::CFC_T1 + 2));
-			V3 t2 = v3(f(o + mbik::CFC_T2), f(o + mbik::CFC_T2 + 1), f(o + mbik::CFC_T2 + 2));
+			auto f3 = [&](int k) { return v3(f(o + k), f(o + k + 1), f(o + k + 2)); };
 			double trcos = soad(t.CD, slot, t.cd_stride, mbik::CD_PER_CONE * i + 1, t.N, s);
-			V3 c = great_tangent_triangle(cp, ncp, t1, t2, f(o + mbik::CFC_ST), f(o + mbik::CFC_CT), trcos, point);
+			V3 c = great_tangent_triangle(f3(mbik::CFC_C1XC2), f3(mbik::CFC_A1), f3(mbik::CFC_A2), f3(mbik::CFC_B1),
+					f3(mbik::CFC_B2), f3(mbik::CFC_T1), f3(mbik::CFC_T2), f(o + mbik::CFC_ST), f(o + mbik::CFC_CT), trcos, point);
 			if (isnan(c.x)) continue;
 			float this_cos = dot(c, point);
 			if (is_equal_approx(this_cos, 1.0f)) {
@@ -1259,7 +1259,7 @@ int32_t mbik_plan_create(const mbik_skeleton_desc *desc, const mbik_config *conf
 	}
 	p->alg_flops = f * h.iterations;
 	p->alg_bytes = (double)h.B * 10 * 4 * 2 + (double)h.P * 12 * 4 + (double)ndir * 9 * 4 +
-			(double)h.NC * (h.cf_stride() * 4.0 + h.cd_stride() * 8.0);
+			(double)h.NC * ((14.0 + 13.0 * h.max_cones) * 4.0 + h.cd_stride() * 8.0); // the per-cone derived constants (CFC_NCP..) excluded
 	h.D.clear(); h.D.shrink_to_fit();
 	h.CF.clear(); h.CF.shrink_to_fit();
 	h.CD.clear(); h.CD.shrink_to_fit();

@@ -99,7 +99,7 @@ class Plan:
         bl = set(describe_topology(parents, pins, constraints, iterations=iterations, default_damp=default_damp,
                                    bone_damp=bone_damp)["bone_list"].tolist())
         self._slots = len({int(c["bone"]) for c in constraints if int(c["bone"]) in bl})
-        self._cf_stride = 14 + 13 * max(1, int(mc))
+        self._cf_stride = 14 + 31 * max(1, int(mc))
         self._cd_stride = 2 * max(1, int(mc))
         self.P = len(pins)
         self.iterations = int(iterations)
