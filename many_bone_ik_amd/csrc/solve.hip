@@ -486,8 +486,10 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, size_t
 			translation = tc - mc;
 		}
 		qrot = qcp_single(mvd, tgt);
-	} else if (m == 1) {
-		// Several headings, one lane: QCP::move_to_weighted_center (qcp.cpp:139-160, float)
+	} else if (m == 1 || nh == 0) {
+		// Several headings (or none: a pinless root segment, whose sums stay zero), one lane or
+		// every lane of the group alike; only nh >= 2 segments own a staged-heading LDS area
+		// (build_schedule).  QCP::move_to_weighted_center (qcp.cpp:139-160, float)
 		// and QCP::inner_product (:162-218, fp64) straight from registers, heading by heading
 		// in the reference's order.  The translate case builds the headings twice, as the
 		// reference's weighted_superpose does.

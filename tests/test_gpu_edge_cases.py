@@ -79,6 +79,18 @@ def test_single_heading_root_segment(oracle, mbik):
     assert_parity(got, ref, "single heading")
 
 
+@pytest.mark.parametrize("lanes", [1, 2, 4, 8, 16])
+def test_pinless_root_segment_beside_pinned_root(oracle, mbik, lanes):
+    """A root segment with no headings sharing a schedule row with a pinned one.  With lane
+    groups of 2+ the headingless segment once took the staged multi-lane QCP path and wrote
+    its exchanged sums past its skeleton's LDS area into the next skeleton's bones."""
+    topo = W.custom_topology([-1, -1, 1, -1, 3, 4], [2, 5], [], iterations=3)
+    wl = W.generate(14, 40, topo=topo)
+    ref = oracle.Oracle(wl).solve(wl.pose, wl.targets)
+    got = Plan.from_workload(wl, lanes=lanes).solve_host(wl.pose, wl.targets)
+    assert_parity(got, ref, f"lanes {lanes}")
+
+
 def test_no_pins_leaves_poses(oracle, mbik):
     topo = W.custom_topology([-1, 0, 1], [], [])
     wl = W.generate(13, 4, topo=topo)
