@@ -42,18 +42,21 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-autotune", action="store_true", help="keep the plan's automatic launch layout")
+    ap.add_argument("--constraint-mode", action="store_true",
+                    help="ManyBoneIK3D::constraint_mode (snaps only; each step is one frame of the persistent node caches)")
+    ap.add_argument("--stabilization-passes", type=int, default=0)
     ap.add_argument("--traffic-json", default=os.path.join(HERE, "profiles", "traffic.json"))
     return ap.parse_args()
 
 
-def cpu_baseline(cfg: int, seconds: float):
+def cpu_baseline(cfg: int, seconds: float, **flags):
     """Oracle (plain-C restatement of the reference) on the host cores, bounded sample."""
     from many_bone_ik_amd import workloads as W
     from oracle import pyoracle as po
     threads = max(1, min(16, os.cpu_count() or 1))
     n = 512 if cfg in (2, 3, 4) else 64
     wl = W.generate(cfg, n)
-    o = po.Oracle(wl)
+    o = po.Oracle(wl, **flags)
     done = 0
     t0 = time.perf_counter()
     while True:
@@ -93,7 +96,8 @@ def main():
     n = args.skeletons or SKEL_PER_GPU[cfg]
     first = rank * n
     wl = W.generate(cfg, n, first=first)
-    plan = Plan.from_workload(wl, device=local_rank, lanes=args.lanes)
+    flags = dict(constraint_mode=args.constraint_mode, stabilization_passes=args.stabilization_passes)
+    plan = Plan.from_workload(wl, device=local_rank, lanes=args.lanes, **flags)
     info = plan.info()
     pose_in = torch.from_numpy(wl.pose).to(dev)
     targets = torch.from_numpy(wl.targets).to(dev)
@@ -163,9 +167,14 @@ def main():
             from oracle import pyoracle as po
             k = min(64, n)
             sub = W.generate(cfg, k, first=first)
-            o = po.Oracle(sub)
+            o = po.Oracle(sub, **flags)
             ref = o.solve(sub.pose, sub.targets, threads=max(1, min(16, os.cpu_count() or 1)))
-            got = pose_out[:k].cpu().numpy()
+            if args.constraint_mode:  # frames advance the node caches: compare a fresh first frame
+                sp = Plan.from_workload(sub, device=local_rank, **flags)
+                got = sp.solve_host(sub.pose, sub.targets)
+                sp.close()
+            else:
+                got = pose_out[:k].cpu().numpy()
             qe = quat_error(got, ref)
             parity = {"skeletons": k, "max_quat_err": float(qe.max()),
                       "frac_skeletons_le_1e-4": float(np.mean(qe.max(-1) <= 1e-4)),
@@ -205,7 +214,9 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (seeded generator, many_bone_ik_amd/workloads.py)",
-        "config": {"workload": W.bench_config_name(cfg), "baseline_config": f"configs[{cfg - 1}]",
+        "config": {"workload": W.bench_config_name(cfg) + (" + constraint_mode" if args.constraint_mode else "") +
+                               (f" + stabilization_passes={args.stabilization_passes}" if args.stabilization_passes else ""),
+                   "baseline_config": f"configs[{cfg - 1}]",
                    "skeletons_per_gpu": n, "bones": wl.bone_count, "effectors": int(wl.topo.pins.shape[0]),
                    "cones_per_bone": wl.topo.cones_per_bone, "iterations": wl.topo.iterations,
                    "lanes_per_skeleton": info["lanes_per_skeleton"], "skeletons_per_block": info["skeletons_per_block"],
@@ -225,7 +236,7 @@ def main():
     }
     if world == 1 and not args.no_cpu_baseline:
         try:
-            out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
+            out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds, **flags)
         except Exception as e:
             out["cpu_baseline"] = {"error": str(e)}
     print(json.dumps(out))

@@ -1,0 +1,348 @@
+// constraint_mode (ManyBoneIK3D::constraint_mode, ik_bone_segment_3d.cpp:142): every bone-step
+// skips the QCP fit and only applies the Kusudama swing and twist snaps.  Included by
+// solve.hip inside its anonymous namespace (DevPlan and the device helpers).
+//
+// Without the fit's set_global_pose nothing refreshes the IKNode3D tree as a whole, so the
+// result depends on which cached globals are stale:
+//   * rotate_local_with_global (the swing snap) dirties only the node it rotates
+//     (ik_node_3d.cpp:56-67), leaving its subtree's caches clean but stale;
+//   * set_transform (the twist snap, the stabilization restore and the frame's pose load)
+//     propagates through the subtree only if the local transform changed (:69-75);
+//   * get_global_transform recomputes a dirty node from its parent, and the parent only if
+//     that is dirty too (:93-113);
+//   * these caches outlive the frame.
+// So this path keeps the reference's node caches themselves: per skeleton, the pose local
+// and the cached globals of the pose, bone-direction, constraint-orientation and twist nodes
+// in HBM (SoA [slot][12][N], persistent across mbik_solve calls), and one dirty bit per node
+// in LDS for the launch (word-packed by pre-order position, so a propagation marks a range).
+// Every node read goes through the same lazy recomputation, in the reference's order.
+// One lane per skeleton: the work is a serial chain per skeleton.
+
+struct CmodeState {
+	float *node;        // [slot][12][N]: pose local (B), pose global (B), bone-direction global (B),
+	                    // constraint-orientation global (NC), twist global (NC)
+	uint32_t *dirty;    // [kind * W + word][N], kinds: pose, bone direction, orientation, twist
+	const int *pre;     // [B] pre-order position in the pose-node forest (list bones)
+	const int *sub;     // [B] subtree size
+	int W;              // dirty words per kind
+	int maxd;           // deepest pose chain
+};
+
+enum { CK_POSE = 0, CK_BDIR = 1, CK_COR = 2, CK_CTW = 3 };
+
+struct CmodeLane {
+	const DevPlan &t;
+	const CmodeState &c;
+	size_t s;             // absolute skeleton index (plan tables)
+	float *node;          // this skeleton's node state: element f of slot k at node[(12 k + f) * fs]
+	size_t fs;            // element stride of the node state (the plan's N)
+	uint32_t *dl;         // this lane's dirty words: dl[(kind * W + w) * ls]
+	int *stk;             // this lane's chain stack: stk[i * ls]
+	int ls;               // lane interleave of the LDS arrays
+	const int *pre, *sub; // LDS copies
+
+	__device__ __forceinline__ float *slot(int k) const { return node + (size_t)k * 12 * fs; }
+	__device__ __forceinline__ X3 ld(int k) const {
+		const float *p = slot(k);
+		const size_t N = fs;
+		X3 x;
+#pragma unroll
+		for (int i = 0; i < 3; i++) x.b.r[i] = v3(p[(3 * i) * N], p[(3 * i + 1) * N], p[(3 * i + 2) * N]);
+		x.o = v3(p[9 * N], p[10 * N], p[11 * N]);
+		return x;
+	}
+	__device__ __forceinline__ void st(int k, const X3 &x) const {
+		float *p = slot(k);
+		const size_t N = fs;
+#pragma unroll
+		for (int i = 0; i < 3; i++) {
+			p[(3 * i) * N] = x.b.r[i].x;
+			p[(3 * i + 1) * N] = x.b.r[i].y;
+			p[(3 * i + 2) * N] = x.b.r[i].z;
+		}
+		p[9 * N] = x.o.x;
+		p[10 * N] = x.o.y;
+		p[11 * N] = x.o.z;
+	}
+	__device__ __forceinline__ int LP(int b) const { return b; }
+	__device__ __forceinline__ int GP(int b) const { return t.B + b; }
+	__device__ __forceinline__ int GD(int b) const { return 2 * t.B + b; }
+	__device__ __forceinline__ int GC(int slot_) const { return 3 * t.B + slot_; }
+	__device__ __forceinline__ int GT(int slot_) const { return 3 * t.B + t.NC + slot_; }
+
+	__device__ __forceinline__ uint32_t &word(int kind, int w) const { return dl[(kind * c.W + w) * ls]; }
+	__device__ __forceinline__ bool dirty(int kind, int b) const {
+		const int p = pre[b];
+		return (word(kind, p >> 5) >> (p & 31)) & 1u;
+	}
+	__device__ __forceinline__ void set_clean(int kind, int b) const {
+		const int p = pre[b];
+		word(kind, p >> 5) &= ~(1u << (p & 31));
+	}
+	__device__ __forceinline__ void set_dirty(int kind, int b) const {
+		const int p = pre[b];
+		word(kind, p >> 5) |= 1u << (p & 31);
+	}
+	__device__ void mark_range(int kind, int lo, int hi) const { // positions [lo, hi)
+		for (int w = lo >> 5; w <= ((hi - 1) >> 5) && lo < hi; w++) {
+			const int a = max(lo, w * 32) - w * 32, z = min(hi, w * 32 + 32) - w * 32; // bits [a, z)
+			const uint32_t m = (z == 32 ? ~0u : ((1u << z) - 1u)) & ~((1u << a) - 1u);
+			word(kind, w) |= m;
+		}
+	}
+	// IKNode3D::_propagate_transform_changed on bone b's pose node (ik_node_3d.cpp:33-49): the
+	// node, its bone-direction child, and every node of the list bones below it.
+	__device__ void propagate(int b) const {
+		const int lo = pre[b], hi = lo + sub[b];
+		mark_range(CK_POSE, lo, hi);
+		mark_range(CK_BDIR, lo, hi);
+		mark_range(CK_COR, lo + 1, hi);
+		mark_range(CK_CTW, lo + 1, hi);
+	}
+
+	// get_global_transform of bone b's pose node (ik_node_3d.cpp:93-113): the dirty chain
+	// above it is recomputed top-down from its first clean ancestor.
+	__device__ X3 pose_global(int b) const {
+		if (!dirty(CK_POSE, b)) return ld(GP(b));
+		int n = 0, x = b, pp;
+		for (;;) {
+			stk[ls * n++] = x;
+			pp = t.bone_pose_parent[x];
+			if (pp < 0 || !dirty(CK_POSE, pp)) break;
+			x = pp;
+		}
+		const X3 Lx = ld(LP(x));
+		X3 G = pp >= 0 ? ld(GP(pp)) * Lx : (pp == mbik::POSE_PARENT_ORIGIN ? xid() * Lx : Lx);
+		st(GP(x), G);
+		set_clean(CK_POSE, x);
+		for (int i = n - 2; i >= 0; i--) {
+			x = stk[ls * i];
+			G = G * ld(LP(x));
+			st(GP(x), G);
+			set_clean(CK_POSE, x);
+		}
+		return G;
+	}
+	// IKBone3D::get_bone_direction_global_pose (ik_bone_3d.cpp:157-159): local = (D, 0).
+	__device__ X3 bdir_global(int b) const {
+		if (!dirty(CK_BDIR, b)) return ld(GD(b));
+		const X3 G = pose_global(b) * X3{ld_soa_basis(t.D, b, 9, 0, t.N, s), v3(0, 0, 0)};
+		st(GD(b), G);
+		set_clean(CK_BDIR, b);
+		return G;
+	}
+	// constraint_orientation_transform: parent = the parent bone's pose node; its local stays
+	// the identity (only set_global_pose copies an origin into it, ik_bone_3d.cpp:145-151).
+	__device__ X3 orient_global(int b) const {
+		const int k = GC(t.bone_cons[b]);
+		if (!dirty(CK_COR, b)) return ld(k);
+		const X3 G = pose_global(t.bone_pose_parent[b]) * xid();
+		st(k, G);
+		set_clean(CK_COR, b);
+		return G;
+	}
+	// constraint_twist_transform: local = (twist frame basis, 0) (ik_kusudama_3d.cpp:37-89).
+	__device__ X3 twist_global(int b) const {
+		const int slot_ = t.bone_cons[b];
+		const int k = GT(slot_);
+		if (!dirty(CK_CTW, b)) return ld(k);
+		const X3 G = pose_global(t.bone_pose_parent[b]) *
+				X3{ld_soa_basis(t.CF, slot_, t.cf_stride, mbik::CF_TWIST_T, t.N, s), v3(0, 0, 0)};
+		st(k, G);
+		set_clean(CK_CTW, b);
+		return G;
+	}
+};
+
+// One constraint_mode bone-step: _qcp_solver's and _set_optimal_rotation's heading builds
+// (ik_bone_segment_3d.cpp:230-231,135,141: only their node reads matter, plus the target
+// headings' origins for stabilization), the swing snap (ik_kusudama_3d.cpp:347-376), the
+// twist snap (:117-132) and, for stabilized root segments, the MSD accept / restore loop
+// (ik_bone_segment_3d.cpp:163-180).  OE: the lane's target-heading origins, OE[ls * (3e + i)].
+template <bool STAB>
+__device__ void cmode_step(const CmodeLane &C, int seg, int k, const float *tg, float *OE, double &prev_dev) {
+	const int ls = C.ls;
+	const DevPlan &t = C.t;
+	const int b = t.seg_bones[k];
+	const int e0 = t.seg_eff_off[seg], e1 = t.seg_eff_off[seg + 1];
+	const bool stab = STAB && (t.seg_flags[seg] & mbik::SF_STAB) != 0;
+	const int flags = t.bone_flags[b];
+	for (int i = e0; i < e1; i++) {
+		const int e = t.seg_effs[i];
+		const X3 E = C.bdir_global(t.eff_bone[e]);
+		if (stab) {
+			OE[ls * (3 * e)] = E.o.x;
+			OE[ls * (3 * e + 1)] = E.o.y;
+			OE[ls * (3 * e + 2)] = E.o.z;
+		}
+	}
+	if (e1 > e0) (void)C.bdir_global(b);
+	const X3 prev = C.ld(C.LP(b));
+	for (int attempt = 0;; attempt++) {
+		if (attempt > 0 && e1 > e0) { // the retry's tip headings (:141)
+			for (int i = e0; i < e1; i++) (void)C.bdir_global(t.eff_bone[t.seg_effs[i]]);
+			(void)C.bdir_global(b);
+		}
+		if (flags & mbik::BF_ORIENT) {
+			const int slot_ = t.bone_cons[b];
+			const X3 Gc = C.orient_global(b);
+			const X3 Gd = C.bdir_global(b);
+			const V3 p1 = Gc.o;
+			const V3 p2 = xform(Gd, v3(0.0f, 1.0f, 0.0f));
+			const V3 tip = xform(affine_inverse(Gc), p2);
+			double in_bounds = 1.0;
+			const V3 inl = local_point_in_limits(t, slot_, C.s, tip, in_bounds);
+			if (in_bounds < 0) {
+				const V3 cp2 = xform(Gc, inl);
+				const Q rect = arc(p2 - p1, cp2 - p1);
+				// rotate_local_with_global (ik_node_3d.cpp:56-67): no propagation
+				const B3 Pb = C.pose_global(t.bone_pose_parent[b]).b;
+				X3 Lb = C.ld(C.LP(b));
+				Lb.b = ((inverse(Pb) * from_quat(rect)) * Pb) * Lb.b;
+				C.st(C.LP(b), Lb);
+				C.set_dirty(CK_POSE, b);
+			}
+		}
+		if (flags & mbik::BF_AXIAL) {
+			const int slot_ = t.bone_cons[b];
+			const int cs = t.cf_stride;
+			const X3 Gt = C.twist_global(b);
+			const X3 Gs = C.pose_global(b);
+			const B3 pgi = inverse(C.pose_global(t.bone_pose_parent[b]).b);
+			const Q tcr = q4(soa(t.CF, slot_, cs, mbik::CF_TWIST_Q, t.N, C.s), soa(t.CF, slot_, cs, mbik::CF_TWIST_Q + 1, t.N, C.s),
+					soa(t.CF, slot_, cs, mbik::CF_TWIST_Q + 2, t.N, C.s), soa(t.CF, slot_, cs, mbik::CF_TWIST_Q + 3, t.N, C.s));
+			const float half_cos = soa(t.CF, slot_, cs, mbik::CF_TWIST_COS, t.N, C.s);
+			const B3 gtc = Gt.b * from_quat(tcr);
+			const B3 align = orthonormalized(inverse(gtc) * Gs.b);
+			Q sw, tw;
+			swing_twist_y(get_rotation_quaternion(align), sw, tw);
+			tw = clamp_cos_half(tw, (double)half_cos);
+			const B3 recomposition = orthonormalized(gtc * from_quat(sw * tw));
+			X3 Lb = C.ld(C.LP(b));
+			const X3 next = {pgi * recomposition, Lb.o};
+			if (!eq(Lb, next)) { // set_transform (ik_node_3d.cpp:69-75)
+				C.st(C.LP(b), next);
+				C.propagate(b);
+			}
+		}
+		if (!stab) break;
+		// _get_manual_msd(tip_headings_uniform, target_headings, weights) (:114-127)
+		const double *hw = t.seg_hw + t.seg_hw_off[seg];
+		float msd = 0.0f;
+		for (int i = e0; i < e1; i++) {
+			const int e = t.seg_effs[i];
+			const X3 E = C.bdir_global(t.eff_bone[e]);
+			const V3 ob = C.bdir_global(b).o;
+			const float *T12 = tg + 12 * e;
+			const X3 T = {bset(T12[0], T12[1], T12[2], T12[3], T12[4], T12[5], T12[6], T12[7], T12[8]), v3(T12[9], T12[10], T12[11])};
+			const V3 oe = v3(OE[ls * (3 * e)], OE[ls * (3 * e + 1)], OE[ls * (3 * e + 2)]);
+			Headings H;
+			heading_terms(t, e, E, T, oe, ob, hw + t.seg_eff_hoff[i], H);
+#pragma unroll
+			for (int h = 0; h < 7; h++) {
+				if (H.mask & (1 << h)) {
+					const V3 d = H.ht[h] - H.hm[h];
+					msd += (float)(H.w[h] * (double)(d.x * d.x + d.y * d.y + d.z * d.z));
+				}
+			}
+		}
+		msd /= t.seg_wsum2[seg];
+		if ((double)msd <= prev_dev * 1.0001) {
+			prev_dev = msd;
+			break;
+		}
+		const X3 Lb = C.ld(C.LP(b));
+		if (!eq(Lb, prev)) { // set_pose(prev_transform): set_transform
+			C.st(C.LP(b), prev);
+			C.propagate(b);
+		}
+		if (attempt + 1 >= t.stab) break;
+	}
+	if (k == t.seg_bone_off[seg + 1] - 1) prev_dev = INFINITY; // the segment root (:178-180)
+}
+
+// _process_modification (many_bone_ik_3d.cpp:645-694) in constraint_mode, one lane per
+// skeleton, 64 skeletons per one-wave block.  LDS: the topology blob, the pre-order tables,
+// then per lane (interleaved by 64): the dirty words (4 W), the chain stack (maxd) and, with
+// STAB, the target-heading origins (3 P).  The node state stays in HBM: staging it through
+// LDS for the launch was measured slower (C2 5.6 vs 5.1 ms, C5 1003 vs 56 ms: the bone-steps
+// are bound by their own dependent arithmetic, and LDS caps how many skeletons are resident;
+// profiles/r01_cmode_layout_sweep.jsonl).
+template <bool STAB>
+__global__ __launch_bounds__(64) void mbik_cmode_kernel(DevPlan t, CmodeState c, int first, int count,
+		const float *__restrict__ pose_in, const float *__restrict__ targets, float *__restrict__ pose_out, int iterations,
+		int seg_lo, int seg_hi) {
+	extern __shared__ float4 lds4[];
+	const int tid = threadIdx.x, nthr = blockDim.x;
+	{
+		uint4 *dst = reinterpret_cast<uint4 *>(lds4);
+		for (int i = tid; i < (t.topo_words >> 2); i += nthr) dst[i] = t.topo_blob[i];
+	}
+	const uint32_t *topo = reinterpret_cast<const uint32_t *>(lds4);
+#define MBIK_REPOINT(T, name) t.name = reinterpret_cast<const T *>(topo + t.o_##name);
+	MBIK_TOPO_TABLES(MBIK_REPOINT)
+#undef MBIK_REPOINT
+	const int B = t.B, P = t.P;
+	int *pre = reinterpret_cast<int *>(lds4) + t.topo_words;
+	int *sub = pre + B;
+	for (int i = tid; i < B; i += nthr) {
+		pre[i] = c.pre[i];
+		sub[i] = c.sub[i];
+	}
+	const int ls = 64;
+	uint32_t *dl0 = reinterpret_cast<uint32_t *>(sub + B);
+	int *stk0 = reinterpret_cast<int *>(dl0 + (size_t)4 * c.W * ls);
+	float *oe0 = reinterpret_cast<float *>(stk0 + (size_t)c.maxd * ls);
+	__syncthreads();
+	const int g = tid;
+	const int local = blockIdx.x * 64 + g;
+	if (local >= count) return; // no barrier below
+	const size_t s = (size_t)first + local;
+	const CmodeLane C{t, c, s, c.node + s, (size_t)t.N, dl0 + g, stk0 + g, ls, pre, sub};
+	for (int w = 0; w < 4 * c.W; w++) C.dl[ls * w] = c.dirty[(size_t)w * t.N + s];
+	float *OE = oe0 + g;
+	// _update_ik_bones_transform (:91-102): set_transform of every list bone's pose
+	for (int b = 0; b < B; b++) {
+		if (!(t.bone_flags[b] & mbik::BF_IN_LIST)) continue;
+		const X3 L = pose_to_xform(pose_in + ((size_t)local * B + b) * 10);
+		if (!eq(C.ld(C.LP(b)), L)) {
+			C.st(C.LP(b), L);
+			C.propagate(b);
+		}
+	}
+	const float *tg = targets + (size_t)local * P * 12;
+	for (int it = 0; it < iterations; it++) {
+		for (int seg = seg_lo; seg <= seg_hi; seg++) {
+			double prev_dev = INFINITY;
+			for (int k = t.seg_bone_off[seg]; k < t.seg_bone_off[seg + 1]; k++) cmode_step<STAB>(C, seg, k, tg, OE, prev_dev);
+		}
+	}
+	for (int b = 0; b < B; b++) {
+		float *dst = pose_out + ((size_t)local * B + b) * 10;
+		if (t.bone_flags[b] & mbik::BF_IN_LIST) {
+			write_pose(C.ld(C.LP(b)), dst);
+		} else {
+			const float *src = pose_in + ((size_t)local * B + b) * 10;
+			for (int f = 0; f < 10; f++) dst[f] = src[f];
+		}
+	}
+	for (int w = 0; w < 4 * c.W; w++) c.dirty[(size_t)w * t.N + s] = C.dl[ls * w];
+}
+
+// A fresh node tree (_bone_list_changed): pose locals = the setup pose, every cache dirty.
+__global__ __launch_bounds__(64) void mbik_cmode_reset_kernel(DevPlan t, CmodeState c, int first, int count,
+		const float *__restrict__ setup_pose) {
+	const int local = blockIdx.x * 64 + threadIdx.x;
+	if (local >= count) return;
+	t.bone_flags = reinterpret_cast<const int *>(reinterpret_cast<const uint32_t *>(t.topo_blob) + t.o_bone_flags);
+	const size_t s = (size_t)first + local;
+	for (int b = 0; b < t.B; b++) {
+		if (!(t.bone_flags[b] & mbik::BF_IN_LIST)) continue;
+		const X3 L = pose_to_xform(setup_pose + ((size_t)local * t.B + b) * 10);
+		float *p = c.node + (size_t)b * 12 * t.N + s;
+		const float v[12] = {L.b.r[0].x, L.b.r[0].y, L.b.r[0].z, L.b.r[1].x, L.b.r[1].y, L.b.r[1].z,
+				L.b.r[2].x, L.b.r[2].y, L.b.r[2].z, L.o.x, L.o.y, L.o.z};
+		for (int f = 0; f < 12; f++) p[(size_t)f * t.N] = v[f];
+	}
+	for (int w = 0; w < 4 * c.W; w++) c.dirty[(size_t)w * t.N + s] = ~0u;
+}

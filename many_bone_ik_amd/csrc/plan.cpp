@@ -301,6 +301,38 @@ std::string build_topology(const mbik_skeleton_desc &desc, const mbik_config &cf
 		p.seg_tin[i] = lo;
 		p.seg_tout[i] = i;
 	}
+	// constraint_mode node caches (cmode.h): pre-order positions over the pose-node forest of
+	// the list bones, so a propagation (IKNode3D::_propagate_transform_changed) marks a range.
+	p.cm_pre.assign(B, -1);
+	p.cm_sub.assign(B, 0);
+	p.cm_maxd = 1;
+	{
+		std::vector<std::vector<int>> pk(B);
+		std::vector<int> roots_in_list;
+		for (int b : p.bone_list) {
+			const int pp = p.bone_pose_parent[b];
+			if (pp >= 0) pk[pp].push_back(b);
+			else roots_in_list.push_back(b);
+		}
+		int pos = 0;
+		std::vector<std::pair<int, int>> stack; // (bone, depth); a negative bone closes -(b+1)
+		for (int r : roots_in_list) {
+			stack.push_back({r, 0});
+			while (!stack.empty()) {
+				auto [b, d] = stack.back();
+				stack.pop_back();
+				if (b < 0) {
+					p.cm_sub[-b - 1] = pos - p.cm_pre[-b - 1];
+					continue;
+				}
+				p.cm_pre[b] = pos++;
+				p.cm_maxd = std::max(p.cm_maxd, d + 1);
+				stack.push_back({-b - 1, d});
+				for (size_t k = pk[b].size(); k-- > 0;) stack.push_back({pk[b][k], d + 1});
+			}
+		}
+		p.cm_npos = pos;
+	}
 	return "";
 }
 

@@ -85,6 +85,10 @@ struct HostPlan {
 	std::vector<int32_t> ik_child_off, ik_children; // IK children of each bone, ascending (setup.h)
 	int32_t setup_max_cones = 1;                    // cones stride of the setup inputs
 	int32_t max_headings = 0;
+	// constraint_mode node caches: pre-order position and subtree size of each list bone in
+	// the pose-node forest (-1 / 0 elsewhere), deepest pose chain, positions used.
+	std::vector<int32_t> cm_pre, cm_sub;
+	int32_t cm_maxd = 1, cm_npos = 0;
 	// ---- launch shape ----
 	int32_t K = 4, log2K = 2, spw = 16;
 	int64_t lds_block_bytes = 0;

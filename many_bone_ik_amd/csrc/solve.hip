@@ -246,6 +246,8 @@ struct Headings {
 	double w[7];
 	int mask;
 };
+__device__ __forceinline__ void heading_terms(const DevPlan &t, int e, const X3 &E, const X3 &T, V3 oe, V3 ob,
+		const double *hw, Headings &H);
 // oe_mode (stabilization, ik_bone_segment_3d.cpp:135-176): 0 plain; 1 also record the target
 // headings' origin in OE; 2 take that origin from OE (target headings are built once per
 // bone-step, before the retry loop, while tip headings are rebuilt on every pass).
@@ -281,7 +283,14 @@ __device__ __forceinline__ void effector_headings(const DevPlan &t, int e, int b
 	} else if (oe_mode == 2) {
 		oe = v3(OE[3 * e], OE[3 * e + 1], OE[3 * e + 2]);
 	}
-	const V3 ob = Gb.o;  // tip headings: the solved bone's origin (:125)
+	heading_terms(t, e, E, T, oe, Gb.o, hw, H);
+}
+
+// The heading pairs of effector e (ik_effector_3d.cpp:90-149): E = the effector bone's
+// bone-direction global, T = its target, oe = the target headings' origin (E.o when built),
+// ob = the solved bone's bone-direction origin (:125).
+__device__ __forceinline__ void heading_terms(const DevPlan &t, int e, const X3 &E, const X3 &T, V3 oe, V3 ob,
+		const double *hw, Headings &H) {
 	H.ht[0] = T.o - oe;
 	H.hm[0] = E.o - ob;
 	H.w[0] = hw[0];
@@ -996,6 +1005,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MBIK_WAVES_P
 #endif
 }
 
+#include "cmode.h"
+
 } // namespace
 
 // ======================================================================================
@@ -1032,6 +1043,8 @@ struct mbik_plan {
 	// device copies of the setup tables (mbik_plan_rebuild_setup)
 	mbik::SetupView dsetup{};
 	bool dsetup_ready = false;
+	// constraint_mode: the persistent IKNode3D caches (cmode.h)
+	CmodeState cm{};
 };
 
 namespace {
@@ -1134,6 +1147,56 @@ int ensure_schedule(mbik_plan *p, int64_t nlaunch) {
 	return MBIK_OK;
 }
 
+// constraint_mode block LDS (cmode.h): topology blob, pre-order tables, then per lane the
+// dirty words, the chain stack and, with stabilization, the target-heading origins.
+size_t cmode_lds_bytes(const mbik_plan *p) {
+	const mbik::HostPlan &h = p->host;
+	return ((size_t)p->dev.topo_words + 2 * (size_t)h.B +
+				   64 * (4 * (size_t)p->cm.W + p->cm.maxd + (h.stabilization_passes > 0 ? 3 * (size_t)h.P : 0))) * sizeof(float);
+}
+
+// Resets the constraint_mode node caches of skeletons [first, first+count) to a fresh tree
+// built on `setup_pose` (device pointer, indexed from `first`).
+int cmode_reset(mbik_plan *p, int first, int count, const float *setup_pose, hipStream_t stream) {
+	if (count <= 0) return MBIK_OK;
+	hipLaunchKernelGGL(mbik_cmode_reset_kernel, dim3((unsigned)((count + 63) / 64)), dim3(64), 0, stream, p->dev, p->cm, first,
+			count, setup_pose);
+	hipError_t e = hipGetLastError();
+	if (e != hipSuccess) return fail(MBIK_EHIP, std::string("constraint_mode reset launch: ") + hipGetErrorString(e));
+	return MBIK_OK;
+}
+
+// constraint_mode: allocates the persistent node caches and builds the fresh tree from the
+// host setup poses of mbik_plan_create.
+int cmode_create(mbik_plan *p, const float *setup_pose) {
+	const mbik::HostPlan &h = p->host;
+	CmodeState &c = p->cm;
+	c.W = std::max(1, (h.cm_npos + 31) / 32);
+	c.maxd = h.cm_maxd;
+	int rc = upload(p, h.cm_pre, c.pre);
+	rc = rc ? rc : upload(p, h.cm_sub, c.sub);
+	if (rc) return rc;
+	const size_t N = (size_t)h.N;
+	const size_t node_bytes = (size_t)(3 * h.B + 2 * h.NC) * 12 * N * sizeof(float);
+	const size_t dirty_bytes = 4 * (size_t)c.W * N * sizeof(uint32_t);
+	void *a = nullptr, *d = nullptr, *sp = nullptr;
+	if (hipMalloc(&a, std::max<size_t>(node_bytes, 4)) != hipSuccess) return fail(MBIK_ENOMEM, "hipMalloc constraint_mode node caches");
+	p->allocs.push_back(a);
+	if (hipMalloc(&d, std::max<size_t>(dirty_bytes, 4)) != hipSuccess) return fail(MBIK_ENOMEM, "hipMalloc constraint_mode dirty bits");
+	p->allocs.push_back(d);
+	p->device_bytes += (int64_t)(node_bytes + dirty_bytes);
+	c.node = static_cast<float *>(a);
+	c.dirty = static_cast<uint32_t *>(d);
+	if (N == 0) return MBIK_OK;
+	const size_t pose_bytes = N * h.B * 10 * sizeof(float);
+	if (hipMalloc(&sp, pose_bytes) != hipSuccess) return fail(MBIK_ENOMEM, "hipMalloc setup pose");
+	rc = hipMemcpy(sp, setup_pose, pose_bytes, hipMemcpyHostToDevice) == hipSuccess ? MBIK_OK : fail(MBIK_EHIP, "hipMemcpy setup pose");
+	if (rc == 0) rc = cmode_reset(p, 0, (int)N, static_cast<const float *>(sp), nullptr);
+	if (rc == 0 && hipDeviceSynchronize() != hipSuccess) rc = fail(MBIK_EHIP, "constraint_mode reset");
+	(void)hipFree(sp);
+	return rc;
+}
+
 int launch(mbik_plan *p, int first, int count, const float *pose_in, const float *targets, float *pose_out,
 		hipStream_t stream, int iterations, int seg_lo, int seg_hi) {
 	if (first < 0 || count < 0 || (int64_t)first + count > p->host.N) return fail(MBIK_EINVAL, "skeleton range out of plan");
@@ -1150,6 +1213,21 @@ int launch(mbik_plan *p, int first, int count, const float *pose_in, const float
 	}
 	int rc = ensure_schedule(p, count);
 	if (rc) return rc;
+	if (h.constraint_mode) {
+		const size_t clds = cmode_lds_bytes(p);
+		if (clds > 160 * 1024) return fail(MBIK_EUNSUPPORTED, "skeleton too large for the constraint_mode LDS layout");
+		static std::once_flag conce;
+		std::call_once(conce, [] {
+			(void)hipFuncSetAttribute((const void *)mbik_cmode_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+			(void)hipFuncSetAttribute((const void *)mbik_cmode_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+		});
+		auto ck = h.stabilization_passes > 0 ? mbik_cmode_kernel<true> : mbik_cmode_kernel<false>;
+		hipLaunchKernelGGL(ck, dim3((unsigned)((count + 63) / 64)), dim3(64), clds, stream, p->dev, p->cm, first, count, pose_in,
+				targets, pose_out, iterations, seg_lo, seg_hi);
+		hipError_t e = hipGetLastError();
+		if (e != hipSuccess) return fail(MBIK_EHIP, std::string("kernel launch failed: ") + hipGetErrorString(e));
+		return MBIK_OK;
+	}
 	size_t lds = ((size_t)h.spw * p->dev.lds_stride + p->dev.topo_words) * sizeof(float);
 	if (lds > 160 * 1024) return fail(MBIK_EUNSUPPORTED, "skeleton too large for LDS at this lane count");
 	static std::once_flag once;
@@ -1196,7 +1274,6 @@ int32_t mbik_plan_create(const mbik_skeleton_desc *desc, const mbik_config *conf
 	int ndev = 0;
 	if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(MBIK_ENODEV, "no HIP device visible");
 	if (device < 0 || device >= ndev) return fail(MBIK_EINVAL, "device index out of range");
-	if (config->constraint_mode) return fail(MBIK_EUNSUPPORTED, "constraint_mode is not implemented on the GPU path yet");
 	std::unique_ptr<mbik_plan> p(new mbik_plan());
 	p->device = device;
 	std::string err = mbik::build_topology(*desc, *config, p->host);
@@ -1230,8 +1307,10 @@ int32_t mbik_plan_create(const mbik_skeleton_desc *desc, const mbik_config *conf
 		return rc;
 	}
 	rc = ensure_schedule(p.get(), n_skeletons);
+	if (rc == 0 && h.constraint_mode) rc = cmode_create(p.get(), setup_pose);
 	if (rc) {
 		for (void *a : p->allocs) (void)hipFree(a);
+		if (p->d_sched) (void)hipFree(p->d_sched);
 		return rc;
 	}
 	// Algorithmic HBM bytes per skeleton, each byte the solve needs read once and each
@@ -1252,7 +1331,7 @@ int32_t mbik_plan_create(const mbik_skeleton_desc *desc, const mbik_config *conf
 		const bool tr = (h.seg_flags[sg] & mbik::SF_TRANSLATE) != 0;
 		for (int k = h.seg_bone_off[sg]; k < h.seg_bone_off[sg + 1]; k++) {
 			const int b = h.seg_bones[k];
-			f += 50.0 * H + (tr ? 14.0 * H : 0.0) + 72.0 * E + 465.0;
+			if (!h.constraint_mode) f += 50.0 * H + (tr ? 14.0 * H : 0.0) + 72.0 * E + 465.0; // no fit in constraint_mode
 			if (h.bone_flags[b] & (mbik::BF_ORIENT | mbik::BF_AXIAL)) {
 				const int C = (h.bone_flags[b] & mbik::BF_ORIENT) ? h.cons_ncones[h.bone_cons[b]] : 0;
 				f += 770.0 + 140.0 * C - 60.0;
@@ -1262,6 +1341,8 @@ int32_t mbik_plan_create(const mbik_skeleton_desc *desc, const mbik_config *conf
 	p->alg_flops = f * h.iterations;
 	p->alg_bytes = (double)h.B * 10 * 4 * 2 + (double)h.P * 12 * 4 + (double)ndir * 9 * 4 +
 			(double)h.NC * ((14.0 + 13.0 * h.max_cones) * 4.0 + h.cd_stride() * 8.0); // the per-cone derived constants (CFC_NCP..) excluded
+	if (h.constraint_mode) // the persistent node caches, read and written once per frame
+		p->alg_bytes += 2.0 * ((double)(3 * h.B + 2 * h.NC) * 12 * 4 + 4.0 * p->cm.W * 4);
 	h.D.clear(); h.D.shrink_to_fit();
 	h.CF.clear(); h.CF.shrink_to_fit();
 	h.CD.clear(); h.CD.shrink_to_fit();
@@ -1291,14 +1372,14 @@ int32_t mbik_plan_get_info(const mbik_plan *p, mbik_plan_info *o) {
 	o->pin_count = h.P;
 	o->segment_count = h.NS;
 	o->level_count = maxh + 1;
-	o->lanes_per_skeleton = h.K;
-	o->skeletons_per_block = h.spw;
+	o->lanes_per_skeleton = h.constraint_mode ? 1 : h.K;
+	o->skeletons_per_block = h.constraint_mode ? 64 : h.spw;
 	o->max_headings = h.max_headings;
 	o->device = p->device;
 	o->device_bytes = p->device_bytes;
 	o->algorithmic_bytes_per_skeleton = p->alg_bytes;
 	o->algorithmic_flops_per_skeleton = p->alg_flops;
-	o->lds_bytes_per_block = p->host.lds_block_bytes;
+	o->lds_bytes_per_block = h.constraint_mode ? (int64_t)cmode_lds_bytes(p) : p->host.lds_block_bytes;
 	return MBIK_OK;
 }
 
@@ -1366,6 +1447,8 @@ int32_t mbik_plan_rebuild_setup(mbik_plan *p, int32_t first, int32_t count, cons
 	(void)hipStreamSynchronize(st);
 	(void)hipFree(scratch);
 	if (e != hipSuccess) return fail(MBIK_EHIP, std::string("setup launch: ") + hipGetErrorString(e));
+	// a rebuilt tree starts with fresh node caches (_bone_list_changed)
+	if (h.constraint_mode) return cmode_reset(p, first, count, setup_pose, st);
 	return MBIK_OK;
 }
 
@@ -1393,6 +1476,9 @@ int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const flo
 		float *pose_out, void *hip_stream) {
 	if (!p) return fail(MBIK_EINVAL, "null plan");
 	if (count <= 0) return MBIK_OK;
+	// constraint_mode has a single layout, and every solve advances the persistent node
+	// caches (a frame): nothing to time, and no solve may run here.
+	if (p->host.constraint_mode) return MBIK_OK;
 	DeviceGuard guard(p->device);
 	hipStream_t st = reinterpret_cast<hipStream_t>(hip_stream);
 	const int lanes = p->lanes_override;

@@ -122,10 +122,14 @@ def test_empty_and_invalid_ranges(mbik):
         plan.set_launch(3)
 
 
-def test_unsupported_flags_fail_loudly(mbik):
-    wl = W.generate(3, 2)
-    t = wl.topo
-    for kw in [dict(constraint_mode=True)]:
-        with pytest.raises(_lib.MbikError) as e:
-            Plan(t.parents, wl.pins(), [], wl.pose, **kw)
-        assert e.value.code == _lib.MBIK_EUNSUPPORTED
+def test_oversized_skeleton_fails_loudly(mbik):
+    """A skeleton whose per-skeleton LDS state cannot fit one block is refused with
+    MBIK_EUNSUPPORTED, never solved some other way."""
+    B = 4000
+    topo = W.custom_topology([-1] + list(range(B - 1)), [B - 1], [], iterations=1)
+    wl = W.generate(3, 1, topo=topo)
+    plan = Plan.from_workload(wl)
+    with pytest.raises(_lib.MbikError) as e:
+        plan.solve_host(wl.pose, wl.targets)
+    assert e.value.code == _lib.MBIK_EUNSUPPORTED
+    plan.close()
