@@ -104,11 +104,16 @@ __device__ __forceinline__ void st_x(float *p, const X3 &t) {
 	*reinterpret_cast<float4 *>(p + 8) = make_float4(t.b.r[2].z, t.o.x, t.o.y, t.o.z);
 }
 // SoA per-skeleton tables: element (item, field) of skeleton s.
+#ifdef MBIK_ABLATE_SOA
+#define MBIK_SOA_S(s) ((s) & 15) // timing experiment only: a hot 16-skeleton working set
+#else
+#define MBIK_SOA_S(s) (s)
+#endif
 __device__ __forceinline__ float soa(const float *a, int item, int fields, int f, int N, size_t s) {
-	return a[((size_t)item * fields + f) * N + s];
+	return a[((size_t)item * fields + f) * N + MBIK_SOA_S(s)];
 }
 __device__ __forceinline__ double soad(const double *a, int item, int fields, int f, int N, size_t s) {
-	return a[((size_t)item * fields + f) * N + s];
+	return a[((size_t)item * fields + f) * N + MBIK_SOA_S(s)];
 }
 __device__ __forceinline__ B3 ld_soa_basis(const float *a, int item, int fields, int f0, int N, size_t s) {
 	B3 b;
