@@ -53,6 +53,7 @@ extern "C" {
 #define MBIK_ABI_VERSION 1
 
 typedef struct mbik_plan mbik_plan;
+typedef struct mbik_group mbik_group;
 
 /* == IKEffectorTemplate3D (src/ik_effector_template_3d.h:40-47). */
 typedef struct mbik_pin {
@@ -151,6 +152,20 @@ int32_t mbik_solve(mbik_plan *plan, int32_t first, int32_t count, const float *p
 /* Same with host buffers; synchronous (copies in, solves, copies out). */
 int32_t mbik_solve_host(mbik_plan *plan, int32_t first, int32_t count, const float *pose_in, const float *targets,
 		float *pose_out);
+/* Heterogeneous batches: several plans (distinct rigs, e.g. a crowd of different characters)
+ * solved by ONE launch, each plan with its own layout.  The reference runs one
+ * ManyBoneIK3D::_process_modification per rig (many_bone_ik_3d.cpp:645-694); a group is
+ * that loop over rigs, fused.  Plans stay owned by the caller and must outlive the group;
+ * all on one device.  constraint_mode and pinless plans run their own launches in order. */
+int32_t mbik_group_create(mbik_plan *const *plans, int32_t n_plans, mbik_group **out_group);
+/* One frame of every plan in the group: per plan i, skeletons [first[i], first[i]+count[i])
+ * (first NULL = 0, count NULL = the plan's skeleton count), device buffers pose_in[i],
+ * targets[i], pose_out[i] as for mbik_solve.  Asynchronous on hip_stream; calls on one group
+ * are stream-ordered (use one stream per group). */
+int32_t mbik_group_solve(mbik_group *group, const int32_t *first, const int32_t *count, const float *const *pose_in,
+		const float *const *targets, float *const *pose_out, void *hip_stream);
+void mbik_group_destroy(mbik_group *group);
+
 /* Runs IKBoneSegment3D::segment_solver() once on `segment` (index in post-order segment
  * numbering of mbik_plan_segment_table) for every skeleton in [first, first+count), updating
  * pose_inout in place (device pointers).  No pose write-back conversion is skipped: the

@@ -915,8 +915,9 @@ __device__ void write_pose(const X3 &t, float *out) {
 #ifndef MBIK_WAVES_PER_EU
 #define MBIK_WAVES_PER_EU 1
 #endif
+// The solve of one block (blk = the plan-local block index after the XCD remap).
 template <bool STAB>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MBIK_WAVES_PER_EU, MBIK_WAVES_PER_EU))) void mbik_solve_kernel(DevPlan t, int first, int count, const float *__restrict__ pose_in,
+__device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int count, const float *__restrict__ pose_in,
 		const float *__restrict__ targets, float *__restrict__ pose_out, int iterations, int seg_lo, int seg_hi) {
 	extern __shared__ float4 lds4[];
 	const int lane = threadIdx.x;
@@ -936,16 +937,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MBIK_WAVES_P
 	float *lds = reinterpret_cast<float *>(lds4) + t.topo_words;
 	const int g = lane >> t.log2K;
 	const int role = lane & (t.K - 1);
-	// XCD-aware block order: the hardware deals consecutive blocks round-robin to the 8
-	// XCDs (separate L2s), so hand each XCD a contiguous run of skeletons; SoA plan rows
-	// of neighbouring skeletons then share cache lines in one L2 instead of eight.
-	const int nb = gridDim.x, nb8 = nb & ~7, bx = blockIdx.x;
-#ifdef MBIK_ABLATE_XCD
-	const int blk = bx;
-	(void)nb8;
-#else
-	const int blk = bx < nb8 ? (bx & 7) * (nb8 >> 3) + (bx >> 3) : bx;
-#endif
 	const int local = blk * t.spw + g;
 	const bool valid = g < t.spw && local < count;
 	const size_t s = (size_t)first + (size_t)(valid ? local : 0);
@@ -1010,6 +1001,50 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MBIK_WAVES_P
 #endif
 }
 
+// XCD-aware block order: the hardware deals consecutive blocks round-robin to the 8 XCDs
+// (separate L2s), so hand each XCD a contiguous run of skeletons; SoA plan rows of
+// neighbouring skeletons then share cache lines in one L2 instead of eight.
+__device__ __forceinline__ int xcd_block() {
+	const int nb = gridDim.x, nb8 = nb & ~7, bx = blockIdx.x;
+#ifdef MBIK_ABLATE_XCD
+	(void)nb8;
+	return bx;
+#else
+	return bx < nb8 ? (bx & 7) * (nb8 >> 3) + (bx >> 3) : bx;
+#endif
+}
+
+template <bool STAB>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MBIK_WAVES_PER_EU, MBIK_WAVES_PER_EU))) void mbik_solve_kernel(DevPlan t, int first, int count, const float *__restrict__ pose_in,
+		const float *__restrict__ targets, float *__restrict__ pose_out, int iterations, int seg_lo, int seg_hi) {
+	solve_block<STAB>(t, xcd_block(), first, count, pose_in, targets, pose_out, iterations, seg_lo, seg_hi);
+}
+
+// A heterogeneous batch (mbik_group_solve): several plans -- distinct rigs -- in one launch.
+// Plan i owns blocks [block_off[i], block_off[i + 1]) of the grid; each block loads its
+// plan's tables and buffers and runs the plan's own layout.
+struct GroupEntry {
+	int block_off, first, count, iterations;
+	const float *pose_in, *targets;
+	float *pose_out;
+};
+template <bool STAB>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MBIK_WAVES_PER_EU, MBIK_WAVES_PER_EU))) void mbik_group_kernel(const DevPlan *__restrict__ plans,
+		const GroupEntry *__restrict__ entries, int n_plans) {
+	// No XCD remap here: the host orders the plans longest chain first, and blocks are
+	// dispatched in grid order, so the long chains start first (LPT) and short rigs fill in.
+	const int gb = blockIdx.x;
+	int lo = 0, hi = n_plans - 1; // the last plan whose first block is <= gb
+	while (lo < hi) {
+		const int mid = (lo + hi + 1) >> 1;
+		if (entries[mid].block_off <= gb) lo = mid;
+		else hi = mid - 1;
+	}
+	DevPlan t = plans[lo];
+	const GroupEntry e = entries[lo];
+	solve_block<STAB>(t, gb - e.block_off, e.first, e.count, e.pose_in, e.targets, e.pose_out, e.iterations, 0, t.NS - 1);
+}
+
 #include "cmode.h"
 
 } // namespace
@@ -1029,6 +1064,12 @@ __global__ __launch_bounds__(64) void mbik_setup_kernel(mbik::SetupView v, int f
 	for (int i = tid; i < count; i += nthreads)
 		mbik::setup_skeleton(v, i, first + i, pose + (size_t)i * v.B * 10, cones, twist, w, D, CF, CD);
 }
+
+struct mbik_group {
+	std::vector<mbik_plan *> plans; // not owned
+	int device = 0;
+	void *d_plans = nullptr, *d_entries = nullptr;
+};
 
 struct mbik_plan {
 	mbik::HostPlan host;
@@ -1565,6 +1606,105 @@ int32_t mbik_segment_solve(mbik_plan *p, int32_t seg, int32_t first, int32_t cou
 	if (seg < 0 || seg >= p->host.NS) return fail(MBIK_EINVAL, "segment out of range");
 	DeviceGuard guard(p->device);
 	return launch(p, first, count, pose_inout, targets, pose_inout, (hipStream_t)stream, 1, p->host.seg_tin[seg], seg);
+}
+
+int32_t mbik_group_create(mbik_plan *const *plans, int32_t n_plans, mbik_group **out_group) {
+	if (!plans || n_plans <= 0 || !out_group) return fail(MBIK_EINVAL, "null argument or empty group");
+	*out_group = nullptr;
+	for (int i = 0; i < n_plans; i++) {
+		if (!plans[i]) return fail(MBIK_EINVAL, "null plan in group");
+		if (plans[i]->device != plans[0]->device) return fail(MBIK_EINVAL, "group plans must share one device");
+	}
+	std::unique_ptr<mbik_group> g(new mbik_group());
+	g->plans.assign(plans, plans + n_plans);
+	g->device = plans[0]->device;
+	DeviceGuard guard(g->device);
+	if (hipMalloc(&g->d_plans, sizeof(DevPlan) * n_plans) != hipSuccess ||
+			hipMalloc(&g->d_entries, sizeof(GroupEntry) * n_plans) != hipSuccess) {
+		if (g->d_plans) (void)hipFree(g->d_plans);
+		return fail(MBIK_ENOMEM, "hipMalloc group tables");
+	}
+	*out_group = g.release();
+	return MBIK_OK;
+}
+
+void mbik_group_destroy(mbik_group *g) {
+	if (!g) return;
+	DeviceGuard guard(g->device);
+	if (g->d_plans) (void)hipFree(g->d_plans);
+	if (g->d_entries) (void)hipFree(g->d_entries);
+	delete g;
+}
+
+int32_t mbik_group_solve(mbik_group *g, const int32_t *first, const int32_t *count, const float *const *pose_in,
+		const float *const *targets, float *const *pose_out, void *hip_stream) {
+	if (!g) return fail(MBIK_EINVAL, "null group");
+	if (!pose_in || !targets || !pose_out) return fail(MBIK_EINVAL, "null buffer array");
+	DeviceGuard guard(g->device);
+	hipStream_t stream = reinterpret_cast<hipStream_t>(hip_stream);
+	const int n = (int)g->plans.size();
+	std::vector<DevPlan> dp;
+	std::vector<GroupEntry> ent;
+	size_t lds = 0;
+	int blocks = 0;
+	bool stab = false;
+	// Longest chain first (iterations x critical-path bone-steps of the plan's schedule).
+	std::vector<std::pair<double, int>> order;
+	for (int i = 0; i < n; i++) {
+		const mbik::HostPlan &h = g->plans[i]->host;
+		double steps = 0;
+		for (int r = 0; r < h.nrows; r++) {
+			int m = 0;
+			for (int l = 0; l < h.K; l++) {
+				const int sg = h.sched[(size_t)r * h.K + l].seg;
+				if (sg >= 0) m = std::max(m, h.seg_bone_off[sg + 1] - h.seg_bone_off[sg]);
+			}
+			steps += m;
+		}
+		order.push_back({-(double)h.iterations * steps, i});
+	}
+	std::stable_sort(order.begin(), order.end());
+	for (auto [key, i] : order) {
+		(void)key;
+		mbik_plan *p = g->plans[i];
+		const int f = first ? first[i] : 0;
+		const int c = count ? count[i] : p->host.N - f;
+		if (f < 0 || c < 0 || (int64_t)f + c > p->host.N) return fail(MBIK_EINVAL, "skeleton range out of plan");
+		if (c == 0) continue;
+		if (!pose_in[i] || !pose_out[i] || (p->host.P > 0 && !targets[i])) return fail(MBIK_EINVAL, "null buffer");
+		if (p->host.constraint_mode || p->host.P == 0) {
+			// constraint_mode plans have their own kernel; pinless plans only copy
+			int rc = launch(p, f, c, pose_in[i], targets[i], pose_out[i], stream, p->host.iterations, 0, p->host.NS - 1);
+			if (rc) return rc;
+			continue;
+		}
+		int rc = ensure_schedule(p, c);
+		if (rc) return rc;
+		const mbik::HostPlan &h = p->host;
+		const size_t l = ((size_t)h.spw * p->dev.lds_stride + p->dev.topo_words) * sizeof(float);
+		if (l > 160 * 1024) return fail(MBIK_EUNSUPPORTED, "skeleton too large for LDS at this lane count");
+		lds = std::max(lds, l);
+		stab = stab || h.stabilization_passes > 0;
+		dp.push_back(p->dev);
+		ent.push_back(GroupEntry{blocks, f, c, h.iterations, pose_in[i], targets[i], pose_out[i]});
+		blocks += (c + h.spw - 1) / h.spw;
+	}
+	if (ent.empty()) return MBIK_OK;
+	if (hipMemcpyAsync(g->d_plans, dp.data(), sizeof(DevPlan) * dp.size(), hipMemcpyHostToDevice, stream) != hipSuccess ||
+			hipMemcpyAsync(g->d_entries, ent.data(), sizeof(GroupEntry) * ent.size(), hipMemcpyHostToDevice, stream) != hipSuccess)
+		return fail(MBIK_EHIP, "hipMemcpyAsync group tables");
+	static std::once_flag once;
+	std::call_once(once, [] {
+		(void)hipFuncSetAttribute((const void *)mbik_group_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+		(void)hipFuncSetAttribute((const void *)mbik_group_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+	});
+	auto kern = stab ? mbik_group_kernel<true> : mbik_group_kernel<false>;
+	hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(64), lds, stream, (const DevPlan *)g->d_plans,
+			(const GroupEntry *)g->d_entries, (int)ent.size());
+	hipError_t e = hipGetLastError();
+	if (e != hipSuccess) return fail(MBIK_EHIP, std::string("group launch failed: ") + hipGetErrorString(e));
+	// the staged tables above are pageable: hipMemcpyAsync has consumed them on return
+	return MBIK_OK;
 }
 
 int32_t mbik_plan_segment_table(const mbik_plan *p, int32_t *root, int32_t *tip, int32_t *parent, int32_t cap) {

@@ -194,6 +194,39 @@ class Plan:
             pass
 
 
+class Group:
+    """mbik_group_*: several plans (distinct rigs) solved by one launch per frame."""
+
+    def __init__(self, plans):
+        self._L = _lib.load()
+        self.plans = list(plans)            # keeps the plans alive while the group exists
+        arr = (C.c_void_p * len(self.plans))(*[p.h for p in self.plans])
+        h = C.c_void_p()
+        check(self._L.mbik_group_create(arr, len(self.plans), C.byref(h)))
+        self.h = h
+
+    def solve(self, pose_in_ptrs, targets_ptrs, pose_out_ptrs, first=None, count=None, stream: int = 0):
+        """Device pointers per plan; first / count: per-plan lists or None (whole plans)."""
+        n = len(self.plans)
+        vpa = C.c_void_p * n
+        i32 = C.c_int32 * n
+        f = i32(*first) if first is not None else None
+        c = i32(*count) if count is not None else None
+        check(self._L.mbik_group_solve(self.h, f, c, vpa(*pose_in_ptrs), vpa(*targets_ptrs), vpa(*pose_out_ptrs),
+                                       C.c_void_p(stream or None)))
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._L.mbik_group_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def quat_error(a: np.ndarray, b: np.ndarray) -> np.ndarray:
     """Per-bone sign-invariant quaternion error min(|q-r|_inf, |q+r|_inf)."""
     qa = a[..., 0:4].astype(np.float64)
