@@ -152,6 +152,17 @@ int32_t mbik_solve(mbik_plan *plan, int32_t first, int32_t count, const float *p
 /* Same with host buffers; synchronous (copies in, solves, copies out). */
 int32_t mbik_solve_host(mbik_plan *plan, int32_t first, int32_t count, const float *pose_in, const float *targets,
 		float *pose_out);
+/* == IKEffector3D::update_target_global_transform for every pin of skeletons [first,
+ * first+count) (ik_effector_3d.cpp:77-84, called by _update_ik_bones_transform,
+ * many_bone_ik_3d.cpp:91-102): targets[s][e] = skeleton_global[s].affine_inverse() *
+ * target_global[s][e] where visible[s][e] != 0 (visible NULL = every target node visible in
+ * the tree); elsewhere targets[s][e] keeps its previous value, as the reference keeps
+ * target_relative_to_skeleton_origin.  Transforms are 12 floats (basis rows, origin):
+ * skeleton_global [count][12], target_global and targets [count][pins][12], visible
+ * [count][pins] bytes; device pointers indexed from `first`, asynchronous on hip_stream. */
+int32_t mbik_capture_targets(mbik_plan *plan, int32_t first, int32_t count, const float *skeleton_global,
+		const float *target_global, const uint8_t *visible, float *targets, void *hip_stream);
+
 /* Heterogeneous batches: several plans (distinct rigs, e.g. a crowd of different characters)
  * solved by ONE launch, each plan with its own layout.  The reference runs one
  * ManyBoneIK3D::_process_modification per rig (many_bone_ik_3d.cpp:645-694); a group is

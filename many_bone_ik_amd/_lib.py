@@ -22,7 +22,7 @@ EXPORTED_SYMBOLS = (
     "mbik_plan_create", "mbik_plan_destroy", "mbik_plan_get_info", "mbik_plan_set_launch", "mbik_plan_set_layout",
     "mbik_plan_autotune", "mbik_plan_resident_blocks", "mbik_plan_rebuild_setup", "mbik_plan_setup_tables",
     "mbik_solve", "mbik_solve_host", "mbik_segment_solve", "mbik_plan_segment_table", "mbik_describe_topology",
-    "mbik_group_create", "mbik_group_solve", "mbik_group_destroy", "mbik_last_error",
+    "mbik_group_create", "mbik_group_solve", "mbik_group_destroy", "mbik_capture_targets", "mbik_last_error",
 )
 
 
@@ -118,6 +118,8 @@ def load():
     L.mbik_group_solve.restype = C.c_int32
     L.mbik_group_destroy.argtypes = [vp]
     L.mbik_group_destroy.restype = None
+    L.mbik_capture_targets.argtypes = [vp, C.c_int32, C.c_int32, vp, vp, vp, vp, vp]
+    L.mbik_capture_targets.restype = C.c_int32
     L.mbik_last_error.argtypes = []
     L.mbik_last_error.restype = C.c_char_p
     _lib = L

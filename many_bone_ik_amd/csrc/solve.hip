@@ -1047,6 +1047,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MBIK_WAVES_P
 
 #include "cmode.h"
 
+// IKEffector3D::update_target_global_transform (ik_effector_3d.cpp:77-84) for a batch: one
+// thread per (skeleton, pin).  Transforms are 12 floats: basis rows, then origin.
+__global__ __launch_bounds__(256) void mbik_capture_targets_kernel(int count, int P, const float *__restrict__ skel_global,
+		const float *__restrict__ target_global, const uint8_t *__restrict__ visible, float *__restrict__ targets) {
+	const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= (int64_t)count * P) return;
+	if (visible && !visible[i]) return; // not visible in tree: the previous target stays
+	const int64_t sk = i / P;
+	const float *a = skel_global + sk * 12, *b = target_global + i * 12;
+	auto xf = [](const float *v) {
+		return X3{bset(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], v[8]), v3(v[9], v[10], v[11])};
+	};
+	const X3 r = affine_inverse(xf(a)) * xf(b);
+	float *o = targets + i * 12;
+	const float w[12] = {r.b.r[0].x, r.b.r[0].y, r.b.r[0].z, r.b.r[1].x, r.b.r[1].y, r.b.r[1].z,
+			r.b.r[2].x, r.b.r[2].y, r.b.r[2].z, r.o.x, r.o.y, r.o.z};
+	for (int f = 0; f < 12; f++) o[f] = w[f];
+}
+
 } // namespace
 
 // ======================================================================================
@@ -1704,6 +1723,22 @@ int32_t mbik_group_solve(mbik_group *g, const int32_t *first, const int32_t *cou
 	hipError_t e = hipGetLastError();
 	if (e != hipSuccess) return fail(MBIK_EHIP, std::string("group launch failed: ") + hipGetErrorString(e));
 	// the staged tables above are pageable: hipMemcpyAsync has consumed them on return
+	return MBIK_OK;
+}
+
+int32_t mbik_capture_targets(mbik_plan *p, int32_t first, int32_t count, const float *skeleton_global,
+		const float *target_global, const uint8_t *visible, float *targets, void *hip_stream) {
+	if (!p) return fail(MBIK_EINVAL, "null plan");
+	if (first < 0 || count < 0 || (int64_t)first + count > p->host.N) return fail(MBIK_EINVAL, "skeleton range out of plan");
+	const int P = p->host.P;
+	if (count == 0 || P == 0) return MBIK_OK;
+	if (!skeleton_global || !target_global || !targets) return fail(MBIK_EINVAL, "null buffer");
+	DeviceGuard guard(p->device);
+	const int64_t n = (int64_t)count * P;
+	hipLaunchKernelGGL(mbik_capture_targets_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+			reinterpret_cast<hipStream_t>(hip_stream), count, P, skeleton_global, target_global, visible, targets);
+	hipError_t e = hipGetLastError();
+	if (e != hipSuccess) return fail(MBIK_EHIP, std::string("capture launch failed: ") + hipGetErrorString(e));
 	return MBIK_OK;
 }
 

@@ -160,6 +160,14 @@ class Plan:
         check(self._L.mbik_solve(self.h, first, count, C.c_void_p(pose_in_ptr), C.c_void_p(targets_ptr),
                                  C.c_void_p(pose_out_ptr), C.c_void_p(stream or None)))
 
+    def capture_targets(self, skeleton_global_ptr: int, target_global_ptr: int, targets_ptr: int,
+                        visible_ptr: int = 0, first: int = 0, count: int | None = None, stream: int = 0):
+        """mbik_capture_targets: skeleton-space targets from scene-space transforms."""
+        count = self.n - first if count is None else count
+        check(self._L.mbik_capture_targets(self.h, first, count, C.c_void_p(skeleton_global_ptr),
+                                           C.c_void_p(target_global_ptr), C.c_void_p(visible_ptr or None),
+                                           C.c_void_p(targets_ptr), C.c_void_p(stream or None)))
+
     def segment_solve(self, segment: int, pose_ptr: int, targets_ptr: int, first: int = 0, count: int | None = None,
                       stream: int = 0):
         count = self.n - first if count is None else count
