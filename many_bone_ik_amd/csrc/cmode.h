@@ -16,7 +16,14 @@
 // in HBM (SoA [slot][12][N], persistent across mbik_solve calls), and one dirty bit per node
 // in LDS for the launch (word-packed by pre-order position, so a propagation marks a range).
 // Every node read goes through the same lazy recomputation, in the reference's order.
-// One lane per skeleton: the work is a serial chain per skeleton.
+//
+// Lanes: K per skeleton, sibling segments of one schedule row (plan.cpp build_schedule) on
+// separate lanes, as in the default kernel.  Sibling segments touch disjoint subtrees, so a
+// lane writes only nodes of its own segment root's subtree (its pre-order range).  A dirty
+// chain that reaches above the segment root is recomputed privately (no write: every sibling
+// would compute the same bits, since nothing above a row changes during it), and the cleaning
+// the reference does at the first such read is applied after the row, one lane at a time.
+// Dirty words are shared by the skeleton's lanes: updates are LDS atomics.
 
 struct CmodeState {
 	float *node;        // [slot][12][N]: pose local (B), pose global (B), bone-direction global (B),
@@ -36,10 +43,12 @@ struct CmodeLane {
 	size_t s;             // absolute skeleton index (plan tables)
 	float *node;          // this skeleton's node state: element f of slot k at node[(12 k + f) * fs]
 	size_t fs;            // element stride of the node state (the plan's N)
-	uint32_t *dl;         // this lane's dirty words: dl[(kind * W + w) * ls]
-	int *stk;             // this lane's chain stack: stk[i * ls]
-	int ls;               // lane interleave of the LDS arrays
+	uint32_t *dl;         // this skeleton's dirty words: dl[(kind * W + w) * dls]
+	int dls;              // their interleave (skeletons per block)
+	int *stk;             // this lane's chain stack: stk[i * 64]
 	const int *pre, *sub; // LDS copies
+	int lo, hi;           // pre-order range this lane may write (its segment root's subtree)
+	int *pend;            // pose node whose dirty chain this lane read privately (-1 none)
 
 	__device__ __forceinline__ float *slot(int k) const { return node + (size_t)k * 12 * fs; }
 	__device__ __forceinline__ X3 ld(int k) const {
@@ -70,26 +79,27 @@ struct CmodeLane {
 	__device__ __forceinline__ int GC(int slot_) const { return 3 * t.B + slot_; }
 	__device__ __forceinline__ int GT(int slot_) const { return 3 * t.B + t.NC + slot_; }
 
-	__device__ __forceinline__ uint32_t &word(int kind, int w) const { return dl[(kind * c.W + w) * ls]; }
+	__device__ __forceinline__ uint32_t *word(int kind, int w) const { return dl + (kind * c.W + w) * dls; }
 	__device__ __forceinline__ bool dirty(int kind, int b) const {
 		const int p = pre[b];
-		return (word(kind, p >> 5) >> (p & 31)) & 1u;
+		return (*word(kind, p >> 5) >> (p & 31)) & 1u;
 	}
 	__device__ __forceinline__ void set_clean(int kind, int b) const {
 		const int p = pre[b];
-		word(kind, p >> 5) &= ~(1u << (p & 31));
+		atomicAnd(word(kind, p >> 5), ~(1u << (p & 31)));
 	}
 	__device__ __forceinline__ void set_dirty(int kind, int b) const {
 		const int p = pre[b];
-		word(kind, p >> 5) |= 1u << (p & 31);
+		atomicOr(word(kind, p >> 5), 1u << (p & 31));
 	}
-	__device__ void mark_range(int kind, int lo, int hi) const { // positions [lo, hi)
-		for (int w = lo >> 5; w <= ((hi - 1) >> 5) && lo < hi; w++) {
-			const int a = max(lo, w * 32) - w * 32, z = min(hi, w * 32 + 32) - w * 32; // bits [a, z)
+	__device__ void mark_range(int kind, int a0, int z0) const { // positions [a0, z0)
+		for (int w = a0 >> 5; w <= ((z0 - 1) >> 5) && a0 < z0; w++) {
+			const int a = max(a0, w * 32) - w * 32, z = min(z0, w * 32 + 32) - w * 32; // bits [a, z)
 			const uint32_t m = (z == 32 ? ~0u : ((1u << z) - 1u)) & ~((1u << a) - 1u);
-			word(kind, w) |= m;
+			atomicOr(word(kind, w), m);
 		}
 	}
+	__device__ __forceinline__ bool owned(int b) const { return pre[b] >= lo && pre[b] < hi; }
 	// IKNode3D::_propagate_transform_changed on bone b's pose node (ik_node_3d.cpp:33-49): the
 	// node, its bone-direction child, and every node of the list bones below it.
 	__device__ void propagate(int b) const {
@@ -102,26 +112,34 @@ struct CmodeLane {
 
 	// get_global_transform of bone b's pose node (ik_node_3d.cpp:93-113): the dirty chain
 	// above it is recomputed top-down from its first clean ancestor.
+	// Nodes outside the lane's range are computed but not written; the lowest such node is
+	// recorded in *pend for the after-row cleaning.
 	__device__ X3 pose_global(int b) const {
 		if (!dirty(CK_POSE, b)) return ld(GP(b));
 		int n = 0, x = b, pp;
 		for (;;) {
-			stk[ls * n++] = x;
+			stk[64 * n++] = x;
 			pp = t.bone_pose_parent[x];
 			if (pp < 0 || !dirty(CK_POSE, pp)) break;
 			x = pp;
 		}
 		const X3 Lx = ld(LP(x));
 		X3 G = pp >= 0 ? ld(GP(pp)) * Lx : (pp == mbik::POSE_PARENT_ORIGIN ? xid() * Lx : Lx);
-		st(GP(x), G);
-		set_clean(CK_POSE, x);
+		keep(x, G);
 		for (int i = n - 2; i >= 0; i--) {
-			x = stk[ls * i];
+			x = stk[64 * i];
 			G = G * ld(LP(x));
-			st(GP(x), G);
-			set_clean(CK_POSE, x);
+			keep(x, G);
 		}
 		return G;
+	}
+	__device__ __forceinline__ void keep(int x, const X3 &G) const {
+		if (owned(x)) {
+			st(GP(x), G);
+			set_clean(CK_POSE, x);
+		} else {
+			*pend = x; // visited top-down: ends as the lowest outside node (the segment root's parent)
+		}
 	}
 	// IKBone3D::get_bone_direction_global_pose (ik_bone_3d.cpp:157-159): local = (D, 0).
 	__device__ X3 bdir_global(int b) const {
@@ -158,10 +176,10 @@ struct CmodeLane {
 // (ik_bone_segment_3d.cpp:230-231,135,141: only their node reads matter, plus the target
 // headings' origins for stabilization), the swing snap (ik_kusudama_3d.cpp:347-376), the
 // twist snap (:117-132) and, for stabilized root segments, the MSD accept / restore loop
-// (ik_bone_segment_3d.cpp:163-180).  OE: the lane's target-heading origins, OE[ls * (3e + i)].
+// (ik_bone_segment_3d.cpp:163-180).  OE: the lane's target-heading origins, OE[64 * (3e + i)].
 template <bool STAB>
 __device__ void cmode_step(const CmodeLane &C, int seg, int k, const float *tg, float *OE, double &prev_dev) {
-	const int ls = C.ls;
+	const int ls = 64;
 	const DevPlan &t = C.t;
 	const int b = t.seg_bones[k];
 	const int e0 = t.seg_eff_off[seg], e1 = t.seg_eff_off[seg + 1];
@@ -261,72 +279,103 @@ __device__ void cmode_step(const CmodeLane &C, int seg, int k, const float *tg, 
 	if (k == t.seg_bone_off[seg + 1] - 1) prev_dev = INFINITY; // the segment root (:178-180)
 }
 
-// _process_modification (many_bone_ik_3d.cpp:645-694) in constraint_mode, one lane per
-// skeleton, 64 skeletons per one-wave block.  LDS: the topology blob, the pre-order tables,
-// then per lane (interleaved by 64): the dirty words (4 W), the chain stack (maxd) and, with
-// STAB, the target-heading origins (3 P).  The node state stays in HBM: staging it through
-// LDS for the launch was measured slower (C2 5.6 vs 5.1 ms, C5 1003 vs 56 ms: the bone-steps
-// are bound by their own dependent arithmetic, and LDS caps how many skeletons are resident;
+// _process_modification (many_bone_ik_3d.cpp:645-694) in constraint_mode: K = 2^log2K lanes
+// per skeleton, 64 / K skeletons per one-wave block, the default kernel's sibling-row
+// schedule (t.sched).  LDS: the topology blob, the pre-order tables, the dirty words (4 W per
+// skeleton, interleaved by skeleton), then per lane (interleaved by 64) the chain stack
+// (maxd) and, with STAB, the target-heading origins (3 P).  The node state stays in HBM:
+// staging it through LDS was measured slower (one lane per skeleton: C2 5.6 vs 5.1 ms, C5
+// 1003 vs 56 ms; LDS caps how many skeletons are resident;
 // profiles/r01_cmode_layout_sweep.jsonl).
 template <bool STAB>
 __global__ __launch_bounds__(64) void mbik_cmode_kernel(DevPlan t, CmodeState c, int first, int count,
 		const float *__restrict__ pose_in, const float *__restrict__ targets, float *__restrict__ pose_out, int iterations,
 		int seg_lo, int seg_hi) {
 	extern __shared__ float4 lds4[];
-	const int tid = threadIdx.x, nthr = blockDim.x;
+	const int lane = threadIdx.x;
 	{
 		uint4 *dst = reinterpret_cast<uint4 *>(lds4);
-		for (int i = tid; i < (t.topo_words >> 2); i += nthr) dst[i] = t.topo_blob[i];
+		for (int i = lane; i < (t.topo_words >> 2); i += 64) dst[i] = t.topo_blob[i];
 	}
 	const uint32_t *topo = reinterpret_cast<const uint32_t *>(lds4);
 #define MBIK_REPOINT(T, name) t.name = reinterpret_cast<const T *>(topo + t.o_##name);
 	MBIK_TOPO_TABLES(MBIK_REPOINT)
 #undef MBIK_REPOINT
-	const int B = t.B, P = t.P;
+	const int B = t.B, P = t.P, K = t.K;
+	const int spw = 64 >> t.log2K;
 	int *pre = reinterpret_cast<int *>(lds4) + t.topo_words;
 	int *sub = pre + B;
-	for (int i = tid; i < B; i += nthr) {
+	for (int i = lane; i < B; i += 64) {
 		pre[i] = c.pre[i];
 		sub[i] = c.sub[i];
 	}
-	const int ls = 64;
 	uint32_t *dl0 = reinterpret_cast<uint32_t *>(sub + B);
-	int *stk0 = reinterpret_cast<int *>(dl0 + (size_t)4 * c.W * ls);
-	float *oe0 = reinterpret_cast<float *>(stk0 + (size_t)c.maxd * ls);
+	int *stk0 = reinterpret_cast<int *>(dl0 + (size_t)4 * c.W * spw);
+	float *OE = reinterpret_cast<float *>(stk0 + (size_t)c.maxd * 64) + lane;
+	const int g = lane >> t.log2K, role = lane & (K - 1);
+	const int local = blockIdx.x * spw + g;
+	const bool valid = local < count;
+	const size_t s = (size_t)first + (valid ? local : 0);
+	int pend = -1;
+	CmodeLane C{t, c, s, c.node + s, (size_t)t.N, dl0 + g, spw, stk0 + lane, pre, sub, 0, 0x7fffffff, &pend};
+	if (valid)
+		for (int w = role; w < 4 * c.W; w += K) C.dl[spw * w] = c.dirty[(size_t)w * t.N + s];
 	__syncthreads();
-	const int g = tid;
-	const int local = blockIdx.x * 64 + g;
-	if (local >= count) return; // no barrier below
-	const size_t s = (size_t)first + local;
-	const CmodeLane C{t, c, s, c.node + s, (size_t)t.N, dl0 + g, stk0 + g, ls, pre, sub};
-	for (int w = 0; w < 4 * c.W; w++) C.dl[ls * w] = c.dirty[(size_t)w * t.N + s];
-	float *OE = oe0 + g;
 	// _update_ik_bones_transform (:91-102): set_transform of every list bone's pose
-	for (int b = 0; b < B; b++) {
-		if (!(t.bone_flags[b] & mbik::BF_IN_LIST)) continue;
-		const X3 L = pose_to_xform(pose_in + ((size_t)local * B + b) * 10);
-		if (!eq(C.ld(C.LP(b)), L)) {
-			C.st(C.LP(b), L);
-			C.propagate(b);
+	if (valid)
+		for (int b = role; b < B; b += K) {
+			if (!(t.bone_flags[b] & mbik::BF_IN_LIST)) continue;
+			const X3 L = pose_to_xform(pose_in + ((size_t)local * B + b) * 10);
+			if (!eq(C.ld(C.LP(b)), L)) {
+				C.st(C.LP(b), L);
+				C.propagate(b);
+			}
 		}
-	}
+	__syncthreads();
 	const float *tg = targets + (size_t)local * P * 12;
 	for (int it = 0; it < iterations; it++) {
-		for (int seg = seg_lo; seg <= seg_hi; seg++) {
-			double prev_dev = INFINITY;
-			for (int k = t.seg_bone_off[seg]; k < t.seg_bone_off[seg + 1]; k++) cmode_step<STAB>(C, seg, k, tg, OE, prev_dev);
+		for (int r = 0; r < t.nrows; r++) {
+			const int4 task = t.sched[r * K + role];
+			if (valid && task.x >= seg_lo && task.x <= seg_hi && task.y == 0) {
+				const int root = t.seg_bones[t.seg_bone_off[task.x + 1] - 1];
+				C.lo = pre[root];
+				C.hi = pre[root] + sub[root];
+				double prev_dev = INFINITY; // reset after the segment root bone (:178-180)
+				for (int k = t.seg_bone_off[task.x]; k < t.seg_bone_off[task.x + 1]; k++)
+					cmode_step<STAB>(C, task.x, k, tg, OE, prev_dev);
+			}
+			__syncthreads();
+			// The cleaning the reference's first read above the segment root did: the dirty
+			// chain from the recorded node up, one lane at a time (siblings share it).
+			uint64_t todo = __ballot(pend >= 0);
+			while (todo) {
+				const int l = __ffsll((unsigned long long)todo) - 1;
+				todo &= todo - 1;
+				if (lane == l) {
+					C.lo = 0;
+					C.hi = 0x7fffffff;
+					(void)C.pose_global(pend);
+					pend = -1;
+				}
+				__threadfence_block();
+			}
+			__syncthreads();
 		}
 	}
-	for (int b = 0; b < B; b++) {
-		float *dst = pose_out + ((size_t)local * B + b) * 10;
-		if (t.bone_flags[b] & mbik::BF_IN_LIST) {
-			write_pose(C.ld(C.LP(b)), dst);
-		} else {
-			const float *src = pose_in + ((size_t)local * B + b) * 10;
-			for (int f = 0; f < 10; f++) dst[f] = src[f];
+	if (valid) {
+		for (int b = role; b < B; b += K) {
+			float *dst = pose_out + ((size_t)local * B + b) * 10;
+			if (t.bone_flags[b] & mbik::BF_IN_LIST) {
+				write_pose(C.ld(C.LP(b)), dst);
+			} else {
+				const float *src = pose_in + ((size_t)local * B + b) * 10;
+				for (int f = 0; f < 10; f++) dst[f] = src[f];
+			}
 		}
 	}
-	for (int w = 0; w < 4 * c.W; w++) c.dirty[(size_t)w * t.N + s] = C.dl[ls * w];
+	__syncthreads();
+	if (valid)
+		for (int w = role; w < 4 * c.W; w += K) c.dirty[(size_t)w * t.N + s] = C.dl[spw * w];
 }
 
 // A fresh node tree (_bone_list_changed): pose locals = the setup pose, every cache dirty.

@@ -1108,8 +1108,9 @@ struct mbik_plan {
 	// device copies of the setup tables (mbik_plan_rebuild_setup)
 	mbik::SetupView dsetup{};
 	bool dsetup_ready = false;
-	// constraint_mode: the persistent IKNode3D caches (cmode.h)
+	// constraint_mode: the persistent IKNode3D caches (cmode.h), lanes per skeleton (0 = auto)
 	CmodeState cm{};
+	int cm_lanes = 0;
 };
 
 namespace {
@@ -1190,10 +1191,18 @@ int blocks_per_cu(void *ctx, int64_t lds_bytes) {
 	return n;
 }
 
+// constraint_mode lanes per skeleton without a measurement: at most 4.  Its bone-steps are
+// cheap and its state lives in HBM, so the chip's VALU issue (many narrow waves), not one
+// skeleton's chain, bounds it beyond that (C2 / C3 / C5: DESIGN.md §1, profiles/r01_cmode_lanes_sweep.jsonl).
+constexpr int kCmodeLanes = 4;
+
 int ensure_schedule(mbik_plan *p, int64_t nlaunch) {
 	mbik::HostPlan &h = p->host;
-	mbik::build_schedule(h, p->lanes_override, nlaunch, p->spw_override, p->interval_override, blocks_per_cu, p,
-			p->cu_count);
+	int lanes = p->lanes_override;
+	if (lanes == 0 && h.constraint_mode && p->cm_lanes > 0) lanes = p->cm_lanes;
+	mbik::build_schedule(h, lanes, nlaunch, p->spw_override, p->interval_override, blocks_per_cu, p, p->cu_count);
+	if (lanes == 0 && h.constraint_mode && h.K > kCmodeLanes)
+		mbik::build_schedule(h, kCmodeLanes, nlaunch, p->spw_override, p->interval_override, blocks_per_cu, p, p->cu_count);
 	if (p->sched_K == h.K && p->sched_c == h.g_interval && p->d_sched) {
 		p->dev.spw = h.spw;
 		return MBIK_OK;
@@ -1212,12 +1221,13 @@ int ensure_schedule(mbik_plan *p, int64_t nlaunch) {
 	return MBIK_OK;
 }
 
-// constraint_mode block LDS (cmode.h): topology blob, pre-order tables, then per lane the
-// dirty words, the chain stack and, with stabilization, the target-heading origins.
+// constraint_mode block LDS (cmode.h): topology blob, pre-order tables, the dirty words of
+// the block's 64 / K skeletons, then per lane the chain stack and, with stabilization, the
+// target-heading origins.
 size_t cmode_lds_bytes(const mbik_plan *p) {
 	const mbik::HostPlan &h = p->host;
-	return ((size_t)p->dev.topo_words + 2 * (size_t)h.B +
-				   64 * (4 * (size_t)p->cm.W + p->cm.maxd + (h.stabilization_passes > 0 ? 3 * (size_t)h.P : 0))) * sizeof(float);
+	return ((size_t)p->dev.topo_words + 2 * (size_t)h.B + (size_t)(64 >> h.log2K) * 4 * p->cm.W +
+				   64 * ((size_t)p->cm.maxd + (h.stabilization_passes > 0 ? 3 * (size_t)h.P : 0))) * sizeof(float);
 }
 
 // Resets the constraint_mode node caches of skeletons [first, first+count) to a fresh tree
@@ -1287,8 +1297,9 @@ int launch(mbik_plan *p, int first, int count, const float *pose_in, const float
 			(void)hipFuncSetAttribute((const void *)mbik_cmode_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 		});
 		auto ck = h.stabilization_passes > 0 ? mbik_cmode_kernel<true> : mbik_cmode_kernel<false>;
-		hipLaunchKernelGGL(ck, dim3((unsigned)((count + 63) / 64)), dim3(64), clds, stream, p->dev, p->cm, first, count, pose_in,
-				targets, pose_out, iterations, seg_lo, seg_hi);
+		const int cspw = 64 >> h.log2K;
+		hipLaunchKernelGGL(ck, dim3((unsigned)((count + cspw - 1) / cspw)), dim3(64), clds, stream, p->dev, p->cm, first, count,
+				pose_in, targets, pose_out, iterations, seg_lo, seg_hi);
 		hipError_t e = hipGetLastError();
 		if (e != hipSuccess) return fail(MBIK_EHIP, std::string("kernel launch failed: ") + hipGetErrorString(e));
 		return MBIK_OK;
@@ -1437,8 +1448,8 @@ int32_t mbik_plan_get_info(const mbik_plan *p, mbik_plan_info *o) {
 	o->pin_count = h.P;
 	o->segment_count = h.NS;
 	o->level_count = maxh + 1;
-	o->lanes_per_skeleton = h.constraint_mode ? 1 : h.K;
-	o->skeletons_per_block = h.constraint_mode ? 64 : h.spw;
+	o->lanes_per_skeleton = h.K;
+	o->skeletons_per_block = h.constraint_mode ? 64 >> h.log2K : h.spw;
 	o->max_headings = h.max_headings;
 	o->device = p->device;
 	o->device_bytes = p->device_bytes;
@@ -1537,15 +1548,73 @@ int32_t mbik_plan_resident_blocks(const mbik_plan *p, int64_t lds_bytes_per_bloc
 	return blocks_per_cu(const_cast<mbik_plan *>(p), lds_bytes_per_block);
 }
 
+// constraint_mode: every solve advances the persistent node caches (a frame), so the caches
+// are saved first, each candidate lane count is timed from that saved state, and the state is
+// put back: the caller's next frame sees the caches as they were.
+static int cmode_autotune(mbik_plan *p, int first, int count, const float *pose_in, const float *targets, float *pose_out,
+		hipStream_t st) {
+	if (p->lanes_override) return MBIK_OK; // pinned by mbik_plan_set_launch / set_layout
+	mbik::HostPlan &h = p->host;
+	// candidates: 1, 2, 4, ... up to the widest sibling level's power of two (the default K)
+	mbik::build_schedule(h, 0, count, 0, 0, blocks_per_cu, p, p->cu_count);
+	const int max_lanes = h.K;
+	const size_t N = (size_t)h.N;
+	const size_t node_bytes = (size_t)(3 * h.B + 2 * h.NC) * 12 * N * sizeof(float);
+	const size_t dirty_bytes = 4 * (size_t)p->cm.W * N * sizeof(uint32_t);
+	void *save = nullptr;
+	if (hipMalloc(&save, node_bytes + dirty_bytes) != hipSuccess) return fail(MBIK_ENOMEM, "hipMalloc autotune state copy");
+	char *sv = static_cast<char *>(save);
+	auto copy = [&](bool to_save) {
+		hipError_t a = to_save ? hipMemcpyAsync(sv, p->cm.node, node_bytes, hipMemcpyDeviceToDevice, st)
+							   : hipMemcpyAsync(p->cm.node, sv, node_bytes, hipMemcpyDeviceToDevice, st);
+		hipError_t b = to_save ? hipMemcpyAsync(sv + node_bytes, p->cm.dirty, dirty_bytes, hipMemcpyDeviceToDevice, st)
+							   : hipMemcpyAsync(p->cm.dirty, sv + node_bytes, dirty_bytes, hipMemcpyDeviceToDevice, st);
+		return a == hipSuccess && b == hipSuccess ? MBIK_OK : fail(MBIK_EHIP, "hipMemcpyAsync autotune state");
+	};
+	hipEvent_t e0, e1;
+	if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) {
+		(void)hipFree(save);
+		return fail(MBIK_EHIP, "hipEventCreate");
+	}
+	int rc = copy(true);
+	float best_ms = 0.0f;
+	int best = 0;
+	for (int lanes = 1; lanes <= max_lanes && rc == MBIK_OK; lanes *= 2) {
+		p->cm_lanes = lanes;
+		if ((rc = ensure_schedule(p, count)) != MBIK_OK) break;
+		float ms = 0.0f;
+		for (int r = 0; r < 3 && rc == MBIK_OK; r++) { // first run warms up, untimed
+			if ((rc = copy(false)) != MBIK_OK) break;
+			(void)hipEventRecord(e0, st);
+			rc = launch(p, first, count, pose_in, targets, pose_out, st, h.iterations, 0, h.NS - 1);
+			(void)hipEventRecord(e1, st);
+			if (rc == MBIK_OK && hipEventSynchronize(e1) != hipSuccess) rc = fail(MBIK_EHIP, "hipEventSynchronize");
+			float t = 0.0f;
+			(void)hipEventElapsedTime(&t, e0, e1);
+			if (r > 0) ms += t;
+		}
+		if (rc == MBIK_OK && (best == 0 || ms < best_ms)) {
+			best_ms = ms;
+			best = lanes;
+		}
+	}
+	if (rc == MBIK_OK) rc = copy(false);
+	if (rc == MBIK_OK && hipStreamSynchronize(st) != hipSuccess) rc = fail(MBIK_EHIP, "hipStreamSynchronize");
+	(void)hipEventDestroy(e0);
+	(void)hipEventDestroy(e1);
+	(void)hipFree(save);
+	p->cm_lanes = best;
+	if (rc != MBIK_OK) return rc;
+	return ensure_schedule(p, count);
+}
+
 int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const float *pose_in, const float *targets,
 		float *pose_out, void *hip_stream) {
 	if (!p) return fail(MBIK_EINVAL, "null plan");
 	if (count <= 0) return MBIK_OK;
-	// constraint_mode has a single layout, and every solve advances the persistent node
-	// caches (a frame): nothing to time, and no solve may run here.
-	if (p->host.constraint_mode) return MBIK_OK;
 	DeviceGuard guard(p->device);
 	hipStream_t st = reinterpret_cast<hipStream_t>(hip_stream);
+	if (p->host.constraint_mode) return cmode_autotune(p, first, count, pose_in, targets, pose_out, st);
 	const int lanes = p->lanes_override;
 	{
 		// A launch whose skeletons are all resident at the default layout is bound by one

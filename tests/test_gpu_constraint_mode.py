@@ -127,3 +127,30 @@ def test_segment_solve(oracle, mbik, torch_dev):
         assert_parity(d.cpu().numpy(), ref, f"segment {seg}")
         pose = ref
     plan.close()
+
+
+def test_autotune_keeps_the_node_caches(oracle, mbik, torch_dev):
+    """mbik_plan_autotune in constraint_mode times lane counts from a saved copy of the node
+    caches and restores it: the frames around it match the oracle's uninterrupted sequence."""
+    torch, dev = torch_dev
+    wl = W.generate(5, 8)
+    ref_o = oracle.Oracle(wl, constraint_mode=True)
+    plan = Plan.from_workload(wl, constraint_mode=True)
+    pose = wl.pose.copy()
+    for f in range(3):
+        if f == 1:
+            pi = torch.from_numpy(pose).to(dev)
+            tg = torch.from_numpy(wl.targets).to(dev)
+            po = torch.empty_like(pi)
+            plan.autotune(pi.data_ptr(), tg.data_ptr(), po.data_ptr())
+            torch.cuda.synchronize()
+        ref = ref_o.solve(pose, wl.targets)
+        got = plan.solve_host(pose, wl.targets)
+        assert_parity(got, ref, f"frame {f}")
+        pose = ref
+    plan.close()
+
+
+@pytest.mark.parametrize("lanes", [1, 2, 4, 8, 16])
+def test_lane_counts(oracle, mbik, lanes):
+    run_frames(oracle, W.generate(5, 6), frames=2, lanes=lanes, seed=60)
