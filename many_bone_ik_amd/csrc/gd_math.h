@@ -37,6 +37,26 @@ GDI float cos_f(float x) { return (float)cos((double)x); }
 GDI float acos_f(float x) { return (float)acos((double)x); }
 #endif
 
+// Square root, correctly rounded (IEEE), as Godot's Math::sqrt(float) on x86.
+// On the device: v_rsq_f64 of the widened input and one fp64 Newton correction, rounded
+// once to float.  tools/sqrt_exhaustive.hip checks all 2^32 inputs against the compiler's
+// correctly rounded sqrtf: identical for every non-NaN result (NaN payloads may differ;
+// NaN-ness does not).  Half the latency of the fp32 sequence (55 vs 107 cycles, same tool).
+#if defined(MBIK_ABLATE_SQRT) && defined(__HIP_DEVICE_COMPILE__)
+GDI float gd_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); } // timing experiment only (1 ulp)
+#elif defined(__HIP_DEVICE_COMPILE__) && !defined(MBIK_IEEE_SQRT)
+GDI float gd_sqrt(float x) {
+	const double xd = x;
+	const double y = __builtin_amdgcn_rsq(xd);
+	const double g = xd * y, h = 0.5 * y;
+	const double e = fma(-g, g, xd);
+	const float r = (float)fma(e, h, g);
+	return __builtin_amdgcn_class(x, 0x260) ? x : r; // +-0 and +inf pass through
+}
+#else
+GDI float gd_sqrt(float x) { return sqrtf(x); }
+#endif
+
 struct V3 {
 	float x, y, z;
 	GDI float operator[](int i) const { return i == 0 ? x : (i == 1 ? y : z); }
@@ -65,12 +85,20 @@ GDI float length_sq(V3 a) {
 	float x2 = a.x * a.x, y2 = a.y * a.y, z2 = a.z * a.z;
 	return x2 + y2 + z2;
 }
-GDI float length(V3 a) { return sqrtf(length_sq(a)); }
+GDI float length(V3 a) { return gd_sqrt(length_sq(a)); }
 GDI V3 normalized(V3 a) {
 	float l = length_sq(a);
 	if (l == 0) return v3(0, 0, 0);
-	float len = sqrtf(l);
+	float len = gd_sqrt(l);
+#ifdef MBIK_ABLATE_NORMDIV
+	float r = 1.0f / len; // timing experiment only
+	return v3(a.x * r, a.y * r, a.z * r);
+#else
+	// IEEE quotients.  A shared fp64 reciprocal ((float)((double)a * r), exact except for
+	// denormal quotients -- tools/div_check.hip) measured slower in the kernel once the
+	// denormal/range guard branch is paid (C2 1.596 vs 1.525 ms).
 	return v3(a.x / len, a.y / len, a.z / len);
+#endif
 }
 GDI bool is_zero_approx(float s) { return fabsf(s) < (float)CMP_EPSILON; }
 GDI bool is_equal_approx(float a, float b) {
@@ -93,7 +121,7 @@ GDI Q q4(float x, float y, float z, float w) { return Q{x, y, z, w}; }
 GDI Q qid() { return Q{0, 0, 0, 1}; }
 GDI float dot(Q a, Q b) { return a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w; }
 GDI Q operator*(Q a, float s) { return q4(a.x * s, a.y * s, a.z * s, a.w * s); }
-GDI Q normalized(Q a) { return a * (1.0f / sqrtf(dot(a, a))); } // operator/ multiplies by 1/s
+GDI Q normalized(Q a) { return a * (1.0f / gd_sqrt(dot(a, a))); } // operator/ multiplies by 1/s
 GDI Q inverse(Q a) { return q4(-a.x, -a.y, -a.z, a.w); }
 GDI Q operator*(Q a, Q b) {
 	float xx = a.w * b.x + a.x * b.w + a.y * b.z - a.z * b.y;
@@ -148,13 +176,13 @@ GDI Q arc(V3 v0, V3 v1) {
 		return q4(a.x, a.y, a.z, 0);
 	}
 	V3 c = cross(n0, n1);
-	float s = sqrtf((1.0f + d) * 2.0f);
+	float s = gd_sqrt((1.0f + d) * 2.0f);
 	float rs = 1.0f / s;
 	return q4(c.x * rs, c.y * rs, c.z * rs, s * 0.5f);
 }
 GDI V3 get_axis(Q q) {
 	if (fabsf(q.w) > 1 - CMP_EPSILON) return v3(q.x, q.y, q.z);
-	float r = 1.0f / sqrtf(1 - q.w * q.w);
+	float r = 1.0f / gd_sqrt(1 - q.w * q.w);
 	return v3(q.x * r, q.y * r, q.z * r);
 }
 GDI float get_angle(Q q) { return 2 * acos_f(q.w); }
@@ -187,24 +215,24 @@ GDI Q get_quaternion(const B3 &m) {
 	float r00 = m.r[0].x, r11 = m.r[1].y, r22 = m.r[2].z;
 	float trace = r00 + r11 + r22;
 	if (trace > 0.0f) {
-		float s = sqrtf(trace + 1.0f);
+		float s = gd_sqrt(trace + 1.0f);
 		float w = s * 0.5f;
 		s = 0.5f / s;
 		return q4((m.r[2].y - m.r[1].z) * s, (m.r[0].z - m.r[2].x) * s, (m.r[1].x - m.r[0].y) * s, w);
 	}
 	int i = r00 < r11 ? (r11 < r22 ? 2 : 1) : (r00 < r22 ? 2 : 0);
 	if (i == 0) { // j = 1, k = 2
-		float s = sqrtf(r00 - r11 - r22 + 1.0f);
+		float s = gd_sqrt(r00 - r11 - r22 + 1.0f);
 		float ti = s * 0.5f;
 		s = 0.5f / s;
 		return q4(ti, (m.r[1].x + m.r[0].y) * s, (m.r[2].x + m.r[0].z) * s, (m.r[2].y - m.r[1].z) * s);
 	} else if (i == 1) { // j = 2, k = 0
-		float s = sqrtf(r11 - r22 - r00 + 1.0f);
+		float s = gd_sqrt(r11 - r22 - r00 + 1.0f);
 		float ti = s * 0.5f;
 		s = 0.5f / s;
 		return q4((m.r[0].y + m.r[1].x) * s, ti, (m.r[2].y + m.r[1].z) * s, (m.r[0].z - m.r[2].x) * s);
 	} else { // i = 2: j = 0, k = 1
-		float s = sqrtf(r22 - r00 - r11 + 1.0f);
+		float s = gd_sqrt(r22 - r00 - r11 + 1.0f);
 		float ti = s * 0.5f;
 		s = 0.5f / s;
 		return q4((m.r[0].z + m.r[2].x) * s, (m.r[1].z + m.r[2].y) * s, ti, (m.r[1].x - m.r[0].y) * s);
@@ -212,6 +240,9 @@ GDI Q get_quaternion(const B3 &m) {
 }
 // Basis::orthonormalize (Gram-Schmidt on columns)
 GDI B3 orthonormalized(const B3 &b) {
+#ifdef MBIK_ABLATE_ORTHO
+	return b; // timing experiment only
+#endif
 	V3 x = col(b, 0), y = col(b, 1), z = col(b, 2);
 	x = normalized(x);
 	y = (y - x * dot(x, y));
@@ -244,6 +275,10 @@ GDI B3 inverse(const B3 &b) {
 // Basis::operator*: (A*B)[i][j] = B[0][j]*A[i][0] + B[1][j]*A[i][1] + B[2][j]*A[i][2]
 GDI B3 operator*(const B3 &a, const B3 &b) {
 	B3 r;
+#ifdef MBIK_ABLATE_MATMUL
+	for (int i = 0; i < 3; i++) r.r[i] = a.r[i] * b.r[i].x; // timing experiment only
+	return r;
+#endif
 #pragma unroll
 	for (int i = 0; i < 3; i++) {
 		V3 ar = a.r[i];

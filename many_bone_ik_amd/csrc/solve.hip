@@ -106,6 +106,8 @@ __device__ __forceinline__ void st_x(float *p, const X3 &t) {
 // SoA per-skeleton tables: element (item, field) of skeleton s.
 #ifdef MBIK_ABLATE_SOA
 #define MBIK_SOA_S(s) ((s) & 15) // timing experiment only: a hot 16-skeleton working set
+#elif defined(MBIK_ABLATE_SOALDS)
+#define MBIK_SOA_S(s) 0 // timing experiment only: skeleton 0's rows, copied into LDS
 #else
 #define MBIK_SOA_S(s) (s)
 #endif
@@ -251,21 +253,48 @@ struct Headings {
 	double w[7];
 	int mask;
 };
-__device__ __forceinline__ void heading_terms(const DevPlan &t, int e, const X3 &E, const X3 &T, V3 oe, V3 ob,
-		const double *hw, Headings &H);
+// Everything an effector's headings read that stays fixed during a solve: its path from the
+// root, its target (skeleton space), the bone-direction basis of its bone, its priorities, and
+// its QCP heading weights in slot order (0 = origin, 1+2a / 2+2a = +/- axis a; 0 when axis a
+// has no priority).  Single-effector segments load it once per segment, not per bone-step.
+struct EffPre {
+	int e, off, de;
+	X3 T;
+	B3 Db;
+	float pr[3];
+	double hws[7];
+};
+__device__ __forceinline__ void load_eff(const DevPlan &t, int e, const float *TG, size_t s, const double *hw, EffPre &p) {
+	p.e = e;
+	p.off = t.eff_path_off[e];
+	p.de = t.eff_path_off[e + 1] - p.off - 1;
+	p.T = ld_x(TG + 12 * e);
+	p.Db = ld_soa_basis(t.D, t.eff_bone[e], 9, 0, t.N, s);
+	p.hws[0] = hw[0];
+	int k = 1;
+#pragma unroll
+	for (int a = 0; a < 3; a++) {
+		p.pr[a] = t.eff_prio[3 * e + a];
+		const bool on = p.pr[a] > 0.0f;
+		p.hws[1 + 2 * a] = on ? hw[k] : 0.0;
+		p.hws[2 + 2 * a] = on ? hw[k + 1] : 0.0;
+		k += on ? 2 : 0;
+	}
+}
+__device__ __forceinline__ void heading_terms(const EffPre &p, const X3 &E, V3 oe, V3 ob, Headings &H);
 // oe_mode (stabilization, ik_bone_segment_3d.cpp:135-176): 0 plain; 1 also record the target
 // headings' origin in OE; 2 take that origin from OE (target headings are built once per
 // bone-step, before the retry loop, while tip headings are rebuilt on every pass).
-__device__ __forceinline__ void effector_headings(const DevPlan &t, int e, int b, const X3 &Gb, const float *L,
-		const float *TG, const float *ST, const int *SF, size_t s, const double *hw, Headings &H, float *OE = nullptr,
-		int oe_mode = 0) {
+__device__ __forceinline__ void effector_headings(const DevPlan &t, const EffPre &p, int b, const X3 &Gb, const float *L,
+		const float *ST, const int *SF, Headings &H, float *OE = nullptr, int oe_mode = 0) {
+	const int e = p.e;
 	X3 E;
 	if (SF[e]) {
 		E = ld_x(ST + 12 * e); // stale bone-direction cache (ik_node_3d.cpp:56-67 never propagates)
 	} else {
 		X3 X = Gb;
-		const int off = t.eff_path_off[e];
-		const int de = t.eff_path_off[e + 1] - off - 1;
+		const int off = p.off;
+		const int de = p.de;
 		int d = t.bone_depth[b] + 1;
 		if (d <= de) {
 			// software-pipelined: the next path bone's local pose loads during this product
@@ -277,39 +306,43 @@ __device__ __forceinline__ void effector_headings(const DevPlan &t, int e, int b
 			}
 			X = X * Ln;
 		}
-		const int eb = t.eff_bone[e];
-		E.b = X.b * ld_soa_basis(t.D, eb, 9, 0, t.N, s);
+		E.b = X.b * p.Db;
 		E.o = X.o;
 	}
-	const X3 T = ld_x(TG + 12 * e);
 	V3 oe = E.o;         // target headings: the effector's own bone origin (:97)
 	if (oe_mode == 1) {
 		OE[3 * e] = oe.x; OE[3 * e + 1] = oe.y; OE[3 * e + 2] = oe.z;
 	} else if (oe_mode == 2) {
 		oe = v3(OE[3 * e], OE[3 * e + 1], OE[3 * e + 2]);
 	}
-	heading_terms(t, e, E, T, oe, Gb.o, hw, H);
+	heading_terms(p, E, oe, Gb.o, H);
+}
+__device__ __forceinline__ void effector_headings(const DevPlan &t, int e, int b, const X3 &Gb, const float *L,
+		const float *TG, const float *ST, const int *SF, size_t s, const double *hw, Headings &H, float *OE = nullptr,
+		int oe_mode = 0) {
+	EffPre p;
+	load_eff(t, e, TG, s, hw, p);
+	effector_headings(t, p, b, Gb, L, ST, SF, H, OE, oe_mode);
 }
 
-// The heading pairs of effector e (ik_effector_3d.cpp:90-149): E = the effector bone's
+// The heading pairs of effector p.e (ik_effector_3d.cpp:90-149): E = the effector bone's
 // bone-direction global, T = its target, oe = the target headings' origin (E.o when built),
 // ob = the solved bone's bone-direction origin (:125).
-__device__ __forceinline__ void heading_terms(const DevPlan &t, int e, const X3 &E, const X3 &T, V3 oe, V3 ob,
-		const double *hw, Headings &H) {
+__device__ __forceinline__ void heading_terms(const EffPre &p, const X3 &E, V3 oe, V3 ob, Headings &H) {
+	const X3 &T = p.T;
 	H.ht[0] = T.o - oe;
 	H.hm[0] = E.o - ob;
-	H.w[0] = hw[0];
+	H.w[0] = p.hws[0];
 	H.mask = 1;
 	double distance = length(ob - T.o);
 	float sb = (float)(distance < 1.0f ? distance : 1.0);
-	int k = 1;
 #pragma unroll
 	for (int a = 0; a < 3; a++) {
-		float pr = t.eff_prio[3 * e + a];
+		float pr = p.pr[a];
 		if (pr > 0.0f) {
-			float w = (float)hw[k];
-			H.w[1 + 2 * a] = hw[k];
-			H.w[2 + 2 * a] = hw[k + 1];
+			float w = (float)p.hws[1 + 2 * a];
+			H.w[1 + 2 * a] = p.hws[1 + 2 * a];
+			H.w[2 + 2 * a] = p.hws[2 + 2 * a];
 			V3 c = col(T.b, a);
 			H.ht[1 + 2 * a] = mulv((c + T.o) - oe, v3(w, w, w));
 			H.ht[2 + 2 * a] = mulv((T.o - c) - oe, v3(w, w, w));
@@ -317,12 +350,30 @@ __device__ __forceinline__ void heading_terms(const DevPlan &t, int e, const X3 
 			H.hm[1 + 2 * a] = ((cm + E.o) - ob) * sb;
 			H.hm[2 + 2 * a] = ((E.o - cm) - ob) * sb;
 			H.mask |= 6 << (2 * a);
-			k += 2;
 		} else {
 			H.w[1 + 2 * a] = H.w[2 + 2 * a] = 0.0;
 			H.ht[1 + 2 * a] = H.ht[2 + 2 * a] = H.hm[1 + 2 * a] = H.hm[2 + 2 * a] = v3(0, 0, 0);
 		}
 	}
+}
+
+// The same for an effector whose target comes from elsewhere (constraint_mode's node caches).
+__device__ __forceinline__ void heading_terms(const DevPlan &t, int e, const X3 &E, const X3 &T, V3 oe, V3 ob,
+		const double *hw, Headings &H) {
+	EffPre p;
+	p.e = e;
+	p.T = T;
+	p.hws[0] = hw[0];
+	int k = 1;
+#pragma unroll
+	for (int a = 0; a < 3; a++) {
+		p.pr[a] = t.eff_prio[3 * e + a];
+		const bool on = p.pr[a] > 0.0f;
+		p.hws[1 + 2 * a] = on ? hw[k] : 0.0;
+		p.hws[2 + 2 * a] = on ? hw[k + 1] : 0.0;
+		k += on ? 2 : 0;
+	}
+	heading_terms(p, E, oe, ob, H);
 }
 
 // IKLimitCone3D::closest_to_cone (ik_open_cone_3d.cpp:358-381)
@@ -443,7 +494,7 @@ __device__ __forceinline__ void qcp_terms(const V3 wc1, const V3 c1, const V3 c2
 // its LDS staging out of the default kernel).
 template <bool STAB>
 __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, size_t s, float *L, const float *G, const float *TG,
-		float *ST, int *SF, float *HS, float *OE, float *MS, double &prev_dev MBIK_PROF_PARAM) {
+		float *ST, int *SF, float *HS, float *OE, float *MS, double &prev_dev, const EffPre &pre, bool hoist MBIK_PROF_PARAM) {
 	MBIK_PROF_T(pt0);
 #ifdef MBIK_PROF
 	uint64_t pt1 = pt0, pt3 = pt0;
@@ -486,7 +537,8 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, size_t
 	Headings H;
 	if (nh == 1) {
 		// one heading in the segment: every lane of the group computes it (qcp.cpp:59-78)
-		effector_headings(t, t.seg_effs[e0], b, Gb, L, TG, ST, SF, s, hw, H, OE, oe_mode);
+		if (hoist) effector_headings(t, pre, b, Gb, L, ST, SF, H, OE, oe_mode);
+		else effector_headings(t, t.seg_effs[e0], b, Gb, L, TG, ST, SF, s, hw, H, OE, oe_mode);
 		V3 mvd = H.hm[0], tgt = H.ht[0];
 		if (translate) {
 			double w = H.w[0];
@@ -511,7 +563,8 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, size_t
 		if (translate) {
 			double wsum = 0;
 			for (int i = e0; i < e1; i++) {
-				effector_headings(t, t.seg_effs[i], b, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, oe_mode);
+				if (hoist) effector_headings(t, pre, b, Gb, L, ST, SF, H, OE, oe_mode);
+				else effector_headings(t, t.seg_effs[i], b, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, oe_mode);
 #pragma unroll
 				for (int h = 0; h < 7; h++) {
 					if (H.mask & (1 << h)) {
@@ -531,7 +584,8 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, size_t
 		const V3 nmc = mc * -1.0f, ntc = tc * -1.0f;
 		for (int i = e0; i < e1; i++) {
 			MBIK_PROF_T(ph1);
-			effector_headings(t, t.seg_effs[i], b, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, oe_mode);
+			if (hoist) effector_headings(t, pre, b, Gb, L, ST, SF, H, OE, oe_mode);
+			else effector_headings(t, t.seg_effs[i], b, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, oe_mode);
 			MBIK_PROF_T(ph2);
 			MBIK_PROF_ADD(9, ph1, ph2);
 #pragma unroll
@@ -935,6 +989,17 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 	MBIK_TOPO_TABLES(MBIK_REPOINT)
 #undef MBIK_REPOINT
 	float *lds = reinterpret_cast<float *>(lds4) + t.topo_words;
+#ifdef MBIK_ABLATE_SOALDS
+	{
+		float *dl = lds + (size_t)t.spw * t.lds_stride;
+		float *cl = dl + t.B * 9;
+		double *xl = reinterpret_cast<double *>(cl + ((t.NC * t.cf_stride + 1) & ~1));
+		for (int i = lane; i < t.B * 9; i += 64) dl[i] = t.D[(size_t)i * t.N + first];
+		for (int i = lane; i < t.NC * t.cf_stride; i += 64) cl[i] = t.CF[(size_t)i * t.N + first];
+		for (int i = lane; i < t.NC * t.cd_stride; i += 64) xl[i] = t.CD[(size_t)i * t.N + first];
+		t.D = dl; t.CF = cl; t.CD = xl; t.N = 1;
+	}
+#endif
 	const int g = lane >> t.log2K;
 	const int role = lane & (t.K - 1);
 	const int local = blk * t.spw + g;
@@ -974,8 +1039,14 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 			const int4 task = t.sched[r * K + role];
 			if (valid && task.x >= seg_lo && task.x <= seg_hi) {
 				double prev_dev = INFINITY; // reset after the segment root bone (:178-180)
-				for (int k = t.seg_bone_off[task.x]; k < t.seg_bone_off[task.x + 1]; k++)
-					bone_step<STAB>(t, task.x, k, task.y, task.z, s, L, G, TG, ST, SF, HS, OE, MS, prev_dev MBIK_PROF_ARG);
+				// A single-effector segment solved by one lane (or with a single heading) reads
+				// the same effector data at every bone-step: load it once for the segment.
+				const int seg = task.x, e0 = t.seg_eff_off[seg];
+				EffPre pre;
+				const bool hoist = !STAB && t.seg_eff_off[seg + 1] - e0 == 1 && (task.z == 1 || t.seg_nh[seg] == 1);
+				if (hoist) load_eff(t, t.seg_effs[e0], TG, s, t.seg_hw + t.seg_hw_off[seg] + t.seg_eff_hoff[e0], pre);
+				for (int k = t.seg_bone_off[seg]; k < t.seg_bone_off[seg + 1]; k++)
+					bone_step<STAB>(t, seg, k, task.y, task.z, s, L, G, TG, ST, SF, HS, OE, MS, prev_dev, pre, hoist MBIK_PROF_ARG);
 			}
 			__syncthreads();
 		}
@@ -1305,6 +1376,9 @@ int launch(mbik_plan *p, int first, int count, const float *pose_in, const float
 		return MBIK_OK;
 	}
 	size_t lds = ((size_t)h.spw * p->dev.lds_stride + p->dev.topo_words) * sizeof(float);
+#ifdef MBIK_ABLATE_SOALDS
+	lds += ((size_t)p->dev.B * 9 + p->dev.NC * p->dev.cf_stride + 2 * p->dev.NC * p->dev.cd_stride + 2) * sizeof(float);
+#endif
 	if (lds > 160 * 1024) return fail(MBIK_EUNSUPPORTED, "skeleton too large for LDS at this lane count");
 	static std::once_flag once;
 	std::call_once(once, [] {
