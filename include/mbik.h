@@ -149,6 +149,13 @@ int32_t mbik_plan_autotune(mbik_plan *plan, int32_t first, int32_t count, const 
  * and pose_out are indexed from skeleton `first`. */
 int32_t mbik_solve(mbik_plan *plan, int32_t first, int32_t count, const float *pose_in, const float *targets,
 		float *pose_out, void *hip_stream);
+/* mbik_solve plus a per-skeleton status byte (device buffer of `count` bytes, indexed from
+ * skeleton `first`): nonfinite[i] = 1 when any bone of skeleton first+i ended the frame with
+ * a non-finite basis, which is written out as the identity rotation exactly as
+ * IKBone3D::set_skeleton_bone_pose does (ik_bone_3d.cpp:174-176); 0 otherwise.  The
+ * reference reports nothing; the flag lets a caller find the skeletons it silently reset. */
+int32_t mbik_solve_checked(mbik_plan *plan, int32_t first, int32_t count, const float *pose_in, const float *targets,
+		float *pose_out, uint8_t *nonfinite, void *hip_stream);
 /* Same with host buffers; synchronous (copies in, solves, copies out). */
 int32_t mbik_solve_host(mbik_plan *plan, int32_t first, int32_t count, const float *pose_in, const float *targets,
 		float *pose_out);
@@ -194,6 +201,12 @@ int32_t mbik_plan_segment_table(const mbik_plan *plan, int32_t *root_bone, int32
 int32_t mbik_describe_topology(const mbik_skeleton_desc *desc, const mbik_config *config, int32_t *bone_list,
 		int32_t *bone_list_count, int32_t *segment_root, int32_t *segment_tip, int32_t *segment_parent,
 		int32_t *segment_headings);
+
+/* Device self-test of the kernel's own float primitives against the compiler's IEEE ones,
+ * over every float bit pattern (2^32 inputs, ~1 s): out[0] = inputs where the solve's square
+ * root differs from the correctly rounded sqrtf (non-NaN results), out[1] = inputs where
+ * exactly one of them is NaN.  Both must be 0 (gd_math.h: gd_sqrt). */
+int32_t mbik_selftest_math(int32_t device, uint64_t out[2]);
 
 const char *mbik_last_error(void);
 

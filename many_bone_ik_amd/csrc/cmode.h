@@ -362,17 +362,19 @@ __global__ __launch_bounds__(64) void mbik_cmode_kernel(DevPlan t, CmodeState c,
 			__syncthreads();
 		}
 	}
+	bool bad = false;
 	if (valid) {
 		for (int b = role; b < B; b += K) {
 			float *dst = pose_out + ((size_t)local * B + b) * 10;
 			if (t.bone_flags[b] & mbik::BF_IN_LIST) {
-				write_pose(C.ld(C.LP(b)), dst);
+				bad |= write_pose(C.ld(C.LP(b)), dst);
 			} else {
 				const float *src = pose_in + ((size_t)local * B + b) * 10;
 				for (int f = 0; f < 10; f++) dst[f] = src[f];
 			}
 		}
 	}
+	write_nonfinite(t, valid, bad, g, role, local);
 	__syncthreads();
 	if (valid)
 		for (int w = role; w < 4 * c.W; w += K) c.dirty[(size_t)w * t.N + s] = C.dl[spw * w];

@@ -82,6 +82,9 @@ struct DevPlan {
 #undef MBIK_DECL
 	const float *D, *CF;
 	const double *CD;
+	// mbik_solve_checked: per-skeleton flag, 1 when any bone's solved basis was non-finite and
+	// was written as the identity rotation (ik_bone_3d.cpp:174-176); null otherwise.
+	unsigned char *nonfinite = nullptr;
 };
 
 // ------------------------------------------------------------------------------------
@@ -953,15 +956,25 @@ __device__ void global_pass(const DevPlan &t, int seg, const float *L, float *G)
 	}
 }
 
-// IKBone3D::set_skeleton_bone_pose (ik_bone_3d.cpp:170-179)
-__device__ void write_pose(const X3 &t, float *out) {
+// IKBone3D::set_skeleton_bone_pose (ik_bone_3d.cpp:170-179); returns whether the basis was
+// non-finite (and replaced by the identity, :174-176).
+__device__ bool write_pose(const X3 &t, float *out) {
 	B3 b = t.b;
-	if (!is_finite(b)) b = bid();
+	const bool bad = !is_finite(b);
+	if (bad) b = bid();
 	Q q = get_rotation_quaternion(b);
 	V3 sc = get_scale(b);
 	out[0] = q.x; out[1] = q.y; out[2] = q.z; out[3] = q.w;
 	out[4] = t.o.x; out[5] = t.o.y; out[6] = t.o.z;
 	out[7] = sc.x; out[8] = sc.y; out[9] = sc.z;
+	return bad;
+}
+// The skeleton's non-finite flag: OR over the K lanes of its group, written by lane role 0.
+__device__ __forceinline__ void write_nonfinite(const DevPlan &t, bool valid, bool bad, int g, int role, int local) {
+	if (!t.nonfinite) return;
+	const unsigned long long bits = __ballot(valid && bad);
+	const unsigned long long mask = t.K >= 64 ? ~0ull : ((1ull << t.K) - 1ull);
+	if (valid && role == 0) t.nonfinite[local] = ((bits >> (g * t.K)) & mask) != 0ull;
 }
 
 // One wave per block, and LDS caps residency at <= 4 blocks per CU (one wave per SIMD), so
@@ -1052,17 +1065,19 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 		}
 	}
 	MBIK_PROF_T(pk2);
+	bool bad = false;
 	if (valid) {
 		for (int b = role; b < B; b += K) {
 			float *dst = pose_out + ((size_t)local * B + b) * 10;
 			if (t.bone_flags[b] & mbik::BF_IN_LIST) {
-				write_pose(ld_x(L + 12 * b), dst);
+				bad |= write_pose(ld_x(L + 12 * b), dst);
 			} else {
 				const float *src = pose_in + ((size_t)local * B + b) * 10;
 				for (int f = 0; f < 10; f++) dst[f] = src[f];
 			}
 		}
 	}
+	write_nonfinite(t, valid, bad, g, role, local);
 	MBIK_PROF_T(pk3);
 	MBIK_PROF_ADD(6, pk2, pk3);
 	MBIK_PROF_ADD(7, pk0, pk3);
@@ -1760,6 +1775,60 @@ int32_t mbik_solve(mbik_plan *p, int32_t first, int32_t count, const float *pose
 	if (!p) return fail(MBIK_EINVAL, "null plan");
 	DeviceGuard guard(p->device);
 	return launch(p, first, count, pose_in, targets, pose_out, (hipStream_t)stream, p->host.iterations, 0, p->host.NS - 1);
+}
+
+} // extern "C"
+namespace {
+__global__ void mbik_selftest_math_kernel(unsigned long long *out) {
+	const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
+	unsigned long long bad = 0, nan_bad = 0;
+	for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (1ull << 32); i += nthreads) {
+		const float x = __uint_as_float((unsigned)i);
+		const float ref = sqrtf(x), got = gd_sqrt(x);
+		const bool rn = ref != ref, gn = got != got;
+		if (rn != gn) nan_bad++;
+		else if (!rn && __float_as_uint(ref) != __float_as_uint(got)) bad++;
+	}
+	if (bad) atomicAdd(&out[0], bad);
+	if (nan_bad) atomicAdd(&out[1], nan_bad);
+}
+} // namespace
+extern "C" {
+
+int32_t mbik_selftest_math(int32_t device, uint64_t out[2]) {
+	if (!out) return fail(MBIK_EINVAL, "null output");
+	int ndev = 0;
+	if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(MBIK_ENODEV, "no HIP device");
+	if (device < 0 || device >= ndev) return fail(MBIK_EINVAL, "device out of range");
+	DeviceGuard guard(device);
+	unsigned long long *d = nullptr;
+	if (hipMalloc(&d, 2 * sizeof(unsigned long long)) != hipSuccess) return fail(MBIK_ENOMEM, "hipMalloc");
+	int rc = MBIK_OK;
+	if (hipMemset(d, 0, 2 * sizeof(unsigned long long)) != hipSuccess) rc = fail(MBIK_EHIP, "hipMemset");
+	if (rc == MBIK_OK) {
+		hipLaunchKernelGGL(mbik_selftest_math_kernel, dim3(8192), dim3(256), 0, 0, d);
+		if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) rc = fail(MBIK_EHIP, "self-test kernel");
+	}
+	unsigned long long h[2] = {0, 0};
+	if (rc == MBIK_OK && hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost) != hipSuccess) rc = fail(MBIK_EHIP, "hipMemcpy");
+	(void)hipFree(d);
+	out[0] = h[0];
+	out[1] = h[1];
+	return rc;
+}
+
+int32_t mbik_solve_checked(mbik_plan *p, int32_t first, int32_t count, const float *pose_in, const float *targets,
+		float *pose_out, uint8_t *nonfinite, void *stream) {
+	if (!p) return fail(MBIK_EINVAL, "null plan");
+	if (!nonfinite) return fail(MBIK_EINVAL, "null nonfinite buffer");
+	DeviceGuard guard(p->device);
+	if (p->host.P == 0 && count > 0 && first >= 0 && (int64_t)first + count <= p->host.N &&
+			hipMemsetAsync(nonfinite, 0, (size_t)count, (hipStream_t)stream) != hipSuccess)
+		return fail(MBIK_EHIP, "hipMemsetAsync");
+	p->dev.nonfinite = nonfinite;
+	const int rc = launch(p, first, count, pose_in, targets, pose_out, (hipStream_t)stream, p->host.iterations, 0, p->host.NS - 1);
+	p->dev.nonfinite = nullptr;
+	return rc;
 }
 
 int32_t mbik_segment_solve(mbik_plan *p, int32_t seg, int32_t first, int32_t count, float *pose_inout, const float *targets,

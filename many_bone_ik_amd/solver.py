@@ -160,6 +160,14 @@ class Plan:
         check(self._L.mbik_solve(self.h, first, count, C.c_void_p(pose_in_ptr), C.c_void_p(targets_ptr),
                                  C.c_void_p(pose_out_ptr), C.c_void_p(stream or None)))
 
+    def solve_checked(self, pose_in_ptr: int, targets_ptr: int, pose_out_ptr: int, nonfinite_ptr: int, first: int = 0,
+                      count: int | None = None, stream: int = 0):
+        """mbik_solve_checked: also writes one byte per skeleton, 1 where a non-finite basis was
+        output as the identity rotation (ik_bone_3d.cpp:174-176)."""
+        count = self.n - first if count is None else count
+        check(self._L.mbik_solve_checked(self.h, first, count, C.c_void_p(pose_in_ptr), C.c_void_p(targets_ptr),
+                                         C.c_void_p(pose_out_ptr), C.c_void_p(nonfinite_ptr), C.c_void_p(stream or None)))
+
     def capture_targets(self, skeleton_global_ptr: int, target_global_ptr: int, targets_ptr: int,
                         visible_ptr: int = 0, first: int = 0, count: int | None = None, stream: int = 0):
         """mbik_capture_targets: skeleton-space targets from scene-space transforms."""

@@ -72,3 +72,42 @@ def test_constraint_mode_degenerate(oracle, mbik):
     wl.pose[3:5, 6, 0] = np.nan
     got, ref = run(oracle, wl, constraint_mode=True)
     assert_equal_nan_aware(got, ref, "constraint_mode degenerate")
+
+
+@pytest.mark.parametrize("constraint_mode", [False, True])
+def test_nonfinite_flags(mbik, constraint_mode):
+    """mbik_solve_checked: the same poses as mbik_solve, plus a byte per skeleton that is 1
+    exactly where a non-finite basis was written as the identity (ik_bone_3d.cpp:174-176)."""
+    import torch
+    dev = torch.device("cuda", 0)
+    wl = W.generate(2, 40)
+    bad = np.array([3, 17, 18, 39])
+    wl.pose[bad, 5, 0] = np.nan  # a NaN rotation: that bone's basis is non-finite throughout
+    pin = torch.from_numpy(wl.pose).to(dev)
+    tg = torch.from_numpy(wl.targets).to(dev)
+    plain = Plan.from_workload(wl, constraint_mode=constraint_mode)
+    checked = Plan.from_workload(wl, constraint_mode=constraint_mode)
+    out0, out1 = torch.empty_like(pin), torch.empty_like(pin)
+    flags = torch.full((wl.n,), 7, dtype=torch.uint8, device=dev)
+    plain.solve(pin.data_ptr(), tg.data_ptr(), out0.data_ptr())
+    checked.solve_checked(pin.data_ptr(), tg.data_ptr(), out1.data_ptr(), flags.data_ptr())
+    torch.cuda.synchronize()
+    assert_equal_nan_aware(out1.cpu().numpy(), out0.cpu().numpy(), "checked vs plain")
+    want = np.zeros(wl.n, np.uint8)
+    want[bad] = 1
+    assert np.array_equal(flags.cpu().numpy(), want)
+    # a sub-range: flags (like the pose buffers) are indexed from `first`
+    f2 = torch.full((8,), 7, dtype=torch.uint8, device=dev)
+    out2 = torch.empty_like(pin)
+    checked2 = Plan.from_workload(wl, constraint_mode=constraint_mode)
+    checked2.solve_checked(pin[12].data_ptr(), tg[12].data_ptr(), out2[12].data_ptr(), f2.data_ptr(), first=12, count=8)
+    torch.cuda.synchronize()
+    assert np.array_equal(f2.cpu().numpy(), want[12:20])
+
+
+def test_selftest_math(mbik):
+    """The solve's square root equals the correctly rounded sqrtf on all 2^32 inputs."""
+    import ctypes
+    out = (ctypes.c_uint64 * 2)()
+    assert mbik.mbik_selftest_math(0, out) == 0
+    assert list(out) == [0, 0]
