@@ -15,7 +15,10 @@ SOURCES = ["solve.hip", "plan.cpp"]
 HEADERS = ["gd_math.h", "plan.h", os.path.join("..", "..", "include", "mbik.h")]
 
 # -ffp-contract=off: every float op rounds separately, as the reference's x86 build does.
-FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
+# -fno-slp-vectorize: the SLP vectorizer's packed fp32 ops cost more register copies than
+# they save in this scalar chain (half the v_mov/v_accvgpr traffic without it; C3 -3%,
+# C2 unchanged; tools/ab_run.sh).
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-slp-vectorize",
          "-Wno-unused-result"]
 
 

@@ -415,8 +415,14 @@ __device__ __forceinline__ V3 great_tangent_triangle(V3 c1xc2, V3 a1, V3 a2, V3 
 	return v3(NAN, NAN, NAN);
 }
 
+#ifndef MBIK_STEP_ATTR
+#define MBIK_STEP_ATTR
+#endif
+#ifndef MBIK_LIMITS_ATTR
+#define MBIK_LIMITS_ATTR
+#endif
 // IKKusudama3D::get_local_point_in_limits (ik_kusudama_3d.cpp:273-332)
-__device__ V3 local_point_in_limits(const DevPlan &t, int slot, size_t s, V3 in_point, double &in_bounds) {
+__device__ MBIK_LIMITS_ATTR V3 local_point_in_limits(const DevPlan &t, int slot, size_t s, V3 in_point, double &in_bounds) {
 	const int nc = t.cons_ncones[slot];
 	V3 point = normalized(in_point);
 	float closest_cos = -2.0f;
@@ -496,7 +502,7 @@ __device__ __forceinline__ void qcp_terms(const V3 wc1, const V3 c1, const V3 c2
 // STAB: the plan has stabilization passes (a separate instantiation keeps the retry loop and
 // its LDS staging out of the default kernel).
 template <bool STAB>
-__device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, size_t s, float *L, const float *G, const float *TG,
+__device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j, int m, size_t s, float *L, const float *G, const float *TG,
 		float *ST, int *SF, float *HS, float *OE, float *MS, double &prev_dev, const EffPre &pre, bool hoist MBIK_PROF_PARAM) {
 	MBIK_PROF_T(pt0);
 #ifdef MBIK_PROF
