@@ -46,6 +46,7 @@ def parse():
                     help="ManyBoneIK3D::constraint_mode (snaps only; each step is one frame of the persistent node caches)")
     ap.add_argument("--stabilization-passes", type=int, default=0)
     ap.add_argument("--traffic-json", default=os.path.join(HERE, "profiles", "traffic.json"))
+    ap.add_argument("--valu-mix-json", default=os.path.join(HERE, "profiles", "valu_mix.json"))
     return ap.parse_args()
 
 
@@ -201,6 +202,17 @@ def main():
                 traffic = tj[key]["hbm_bytes_per_launch"]
         except Exception:
             traffic = None
+    issue = None  # the single-wave VALU issue ceiling, from the committed PMC passes
+    if os.path.exists(args.valu_mix_json):
+        try:
+            vm = json.load(open(args.valu_mix_json)).get(f"c{cfg}_{n}")
+            if vm:
+                issue = {"bound": "valu_issue_1wave", "achieved_cycles_per_wave": vm["valu_issue_floor_cycles"],
+                         "wave_cycles": vm["wave_cycles"], "frac": vm["issue_frac"],
+                         "note": "4 cycles per wave64 VALU instruction x VALU instructions / wave cycles (PMC, "
+                                 "profiles/valu_mix.json); the ceiling this latency-bound chain runs against"}
+        except Exception:
+            issue = None
     out = {
         "metric": METRIC,
         "value": value,
@@ -230,6 +242,7 @@ def main():
                  "frac": alg_flops / (kernel_ms * 1e-3) / 1e12 / VALU_PEAK_TFLOPS,
                  "algorithmic_flops_per_launch": alg_flops,
                  "note": "SURVEY.md §8(d) flop formula; the bound that applies to this path (DESIGN.md §5)"},
+        "issue": issue,
         "gather_ms": gather_ms,
         "pcie_inclusive": pcie,
         "parity": parity,
