@@ -138,3 +138,46 @@ def test_rig_loaded_from_scene_properties(oracle, mbik):
                         default_damp=ik.get_default_damp()).solve(wl.pose, wl.targets)
     got = ik.process_modification(wl.pose, wl.targets)
     assert_parity(got, ref, "scene-configured rig")
+
+
+@pytest.mark.parametrize("priorities", ["none", "default", "all_axes"])
+@pytest.mark.parametrize("constrained", [False, True])
+def test_exact_geometry_qcp_branches(oracle, mbik, priorities, constrained):
+    """Axis-aligned rigs with targets placed on exact geometric coincidences, so that QCP's
+    special branches run with exactly representable inputs (qcp.cpp:59-78, :107-109):
+    antiparallel single pairs (a 180-degree arc about the moved heading itself), zero-length
+    target or tip headings (identity), targets already reached (all headings aligned), and
+    targets whose basis is turned half a turn (antiparallel axis headings)."""
+    parents = [-1, 0, 1, 2, 0, 4, 5]
+    cons = [1, 2, 3, 4, 5, 6] if constrained else []
+    topo = W.custom_topology(parents, [3, 6], cons, cones_per_bone=2 if constrained else 0,
+                             twist=(0.0, math.tau) if constrained else None, iterations=6)
+    n = 8
+    wl = W.generate(15, n, topo=topo)
+    wl.pose[:] = 0.0
+    wl.pose[..., 3] = 1.0                      # identity rotations
+    wl.pose[:, 1:, 5] = 1.0                    # unit bones along +Y
+    wl.pose[..., 7:10] = 1.0
+    eye = np.eye(3, dtype=np.float32).reshape(9)
+    half_y = np.diag([-1.0, 1.0, -1.0]).astype(np.float32).reshape(9)
+    fk = {3: (0.0, 3.0, 0.0), 6: (0.0, 3.0, 0.0)}
+    # per skeleton: (pin-3 origin, pin-3 basis, pin-6 origin, pin-6 basis)
+    layouts = [
+        ((0, 2.5, 0), eye, fk[6], eye),        # pin 3 behind its bone: antiparallel pair for bone 2
+        ((0, 2.0, 0), eye, (0, 0, 0), eye),    # targets on bone origins / the root origin
+        (fk[3], eye, fk[6], eye),              # already reached
+        (fk[3], half_y, fk[6], half_y),        # reached, basis half a turn about Y
+        ((0, -1.0, 0), eye, (0, 3.0, 0), half_y),
+        ((0, 3.0, 0), half_y, (0, 2.5, 0), eye),
+        ((0, 1.0, 0), eye, (0, 1.0, 0), eye),  # on bone 1 / bone 4 origins
+        ((0, 4.0, 0), eye, (0, 4.0, 0), half_y),  # straight ahead: aligned, beyond reach
+    ]
+    for s, (o3, b3, o6, b6) in enumerate(layouts):
+        wl.targets[s, 0, :9], wl.targets[s, 0, 9:] = b3, o3
+        wl.targets[s, 1, :9], wl.targets[s, 1, 9:] = b6, o6
+    if priorities == "none":
+        with_pins(wl, pin_priority=np.zeros((2, 3)))
+    elif priorities == "all_axes":
+        with_pins(wl, pin_priority=np.ones((2, 3)))
+    got, ref = run(oracle, wl)
+    assert_parity(got, ref, f"exact geometry {priorities} constrained={constrained}")
