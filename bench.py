@@ -194,10 +194,13 @@ def main():
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
     alg_flops = info["algorithmic_flops_per_skeleton"] * n
     traffic = None
+    # committed PMC evidence is keyed by config, size and kernel variant (the plain solve has
+    # no suffix): a constraint_mode or stabilization run never borrows the plain kernel's
+    key = f"c{cfg}_{n}" + ("_cmode" if args.constraint_mode else "") + \
+        (f"_stab{args.stabilization_passes}" if args.stabilization_passes else "")
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
-            key = f"c{cfg}_{n}"
             if key in tj:
                 traffic = tj[key]["hbm_bytes_per_launch"]
         except Exception:
@@ -205,7 +208,7 @@ def main():
     issue = None  # the single-wave VALU issue ceiling, from the committed PMC passes
     if os.path.exists(args.valu_mix_json):
         try:
-            vm = json.load(open(args.valu_mix_json)).get(f"c{cfg}_{n}")
+            vm = json.load(open(args.valu_mix_json)).get(key)
             if vm:
                 issue = {"bound": "valu_issue_1wave", "achieved_cycles_per_wave": vm["valu_issue_floor_cycles"],
                          "wave_cycles": vm["wave_cycles"], "frac": vm["issue_frac"],
