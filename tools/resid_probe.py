@@ -1,3 +1,4 @@
+"""Residency (one-wave blocks per CU) the occupancy query reports for each LDS size of a plan."""
 import sys
 sys.path.insert(0, '.')
 from many_bone_ik_amd import workloads as W

@@ -1,4 +1,5 @@
 #!/bin/bash
+# PMC latency/level counters (LDS, VMEM, SMEM) of the solve kernel: CFG=<cfg> tools/sq_latency.sh
 set -e
 cd "$(dirname "$0")/.."
 ROOT=$PWD
