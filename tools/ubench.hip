@@ -1,6 +1,6 @@
 // Single-wave instruction cost micro-benchmark (one wave per CU, s_memtime around a loop of
 // N repetitions): how many cycles one wave's dependent / independent streams of the solve
-// kernel.s building blocks cost on gfx950.
+// kernel's building blocks cost on gfx950.
 //   hipcc --offload-arch=gfx950 -O3 -ffp-contract=off tools/ubench.hip -o build/ubench
 #include <hip/hip_runtime.h>
 #include <cmath>
