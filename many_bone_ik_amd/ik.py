@@ -35,6 +35,9 @@ class ManyBoneIK3D:
         self.bone_damp: list[float] = []
         # pins: IKEffectorTemplate3D defaults (ik_effector_template_3d.h:40-47)
         self._pins: list[dict] = []
+        self._pin_count = 0          # pin_count: set_pin_count changes it without resizing pins (:58-60)
+        self.ui_selected_bone = -1   # many_bone_ik_3d.h: editor selection, stored only
+        self.node_exists = lambda path: True   # scene-tree lookup for set_effector_pin_node_path
         # constraints (many_bone_ik_3d.cpp:467-490 defaults for new entries)
         self._constraints: list[dict] = []
         self._plan: Plan | None = None
@@ -52,14 +55,37 @@ class ManyBoneIK3D:
 
     # ----------------------------------------------------------------- pins
     def set_total_effector_count(self, count: int):       # many_bone_ik_3d.cpp:44-52
+        self._pin_count = int(count)
         while len(self._pins) < count:
             self._pins.append(dict(name="", weight=0.0, direction_priorities=(0.2, 0.0, 0.2),
                                    motion_propagation_factor=1.0, target_node=""))
         del self._pins[count:]
         self.set_dirty()
 
-    def get_effector_count(self) -> int:
-        return len(self._pins)
+    def get_effector_count(self) -> int:                  # :54-56 (pin_count, not pins.size())
+        return self._pin_count
+
+    def set_effector_count(self, count: int):             # :58-60: the count only, no resize, not dirty
+        self._pin_count = int(count)
+
+    get_pin_count = get_effector_count                    # bound names (:400-401)
+    set_pin_count = set_effector_count
+
+    def find_pin(self, name: str) -> int:                 # :986-993, over pin_count
+        for i in range(self._pin_count):
+            if self.get_effector_bone_name(i) == name:
+                return i
+        return -1
+
+    def get_pin_enabled(self, i: int) -> bool:            # :911-918: true for any valid index
+        return 0 <= i < len(self._pins)
+
+    def set_effector_pin_node_path(self, i: int, path: str):   # :629-637: only a path that resolves
+        if 0 <= i < len(self._pins) and self.node_exists(path):
+            self._pins[i]["target_node"] = str(path)
+
+    def get_effector_pin_node_path(self, i: int) -> str:  # :639-643
+        return self._pins[i]["target_node"] if 0 <= i < len(self._pins) else ""
 
     def set_effector_bone_name(self, i: int, bone: str):
         if 0 <= i < len(self._pins):
@@ -110,6 +136,19 @@ class ManyBoneIK3D:
 
     def get_constraint_count(self) -> int:
         return len(self._constraints)
+
+    set_constraint_count = _set_constraint_count          # bound name (:417)
+
+    def find_constraint(self, name: str) -> int:          # :734-741
+        for i, c in enumerate(self._constraints):
+            if c["name"] == name:
+                return i
+        return -1
+
+    def remove_constraint_at_index(self, i: int):         # :743-754
+        if 0 <= i < len(self._constraints):
+            del self._constraints[i]
+            self.set_dirty()
 
     def set_constraint_name_at_index(self, i: int, name: str):
         if 0 <= i < len(self._constraints):
@@ -179,6 +218,49 @@ class ManyBoneIK3D:
 
     def get_joint_twist(self, i: int):
         return self._constraints[i]["twist"] if 0 <= i < len(self._constraints) else (0.0, 0.0)
+
+    # ----------------------------------------------------------------- bone damp / reset
+    def _set_bone_count(self, count: int):                # :756-764: new entries take default_damp
+        while len(self.bone_damp) < count:
+            self.bone_damp.append(self.default_damp)
+        del self.bone_damp[count:]
+        self.set_dirty()
+
+    def get_bone_count(self) -> int:                      # :766-768
+        return len(self.bone_damp)
+
+    def reset_constraints(self):                          # :927-940 (the skeleton is always present)
+        pins, cons = self._pin_count, len(self._constraints)
+        self.set_total_effector_count(0)
+        self.set_total_effector_count(pins)
+        self._set_constraint_count(0)
+        self._set_constraint_count(cons)
+        self._set_bone_count(0)
+        self._set_bone_count(cons)
+        self.set_dirty()
+
+    def register_skeleton(self):                          # :920-925
+        if not self.get_effector_count() and not self.get_constraint_count():
+            self.reset_constraints()
+        self.set_dirty()
+
+    def set_ui_selected_bone(self, bone: int):            # :950-956 (editor state, stored only)
+        self.ui_selected_bone = int(bone)
+
+    def get_ui_selected_bone(self) -> int:
+        return self.ui_selected_bone
+
+    # The per-bone IKNode3D transforms of the built tree (:774-909) are editor-gizmo accessors
+    # of the reference's live object graph.  Here the tree lives on the device as the plan's
+    # setup tables (mbik_plan_setup_tables); editing a node transform in place is not part of
+    # the solve path this package replaces.
+    def _tree_accessor(self, *_):
+        raise NotImplementedError("IKNode3D transform accessors of the built tree are editor-gizmo helpers; "
+                                  "read the plan's setup tables with Plan.setup_tables() (DESIGN.md §9)")
+
+    get_twist_transform_of_constraint = set_twist_transform_of_constraint = _tree_accessor
+    get_orientation_transform_of_constraint = set_orientation_transform_of_constraint = _tree_accessor
+    get_direction_transform_of_bone = set_direction_transform_of_bone = _tree_accessor
 
     # ----------------------------------------------------------------- solver properties
     def set_iterations_per_frame(self, n):
@@ -266,7 +348,7 @@ class ManyBoneIK3D:
         rebuilt from pose_in when dirty, exactly when the reference calls _bone_list_changed.
         """
         pose_in = np.ascontiguousarray(pose_in, np.float32)
-        if not self._pins:                        # get_effector_count() == 0: no-op
+        if self.get_effector_count() == 0 or not self._pins:   # :649-651 and the has_pins check (:669-678)
             return pose_in.copy()
         if self._dirty or self._plan is None or self._plan.n != pose_in.shape[0]:
             self._bone_list_changed(pose_in, cones, twist)
