@@ -121,6 +121,12 @@ int32_t mbik_plan_set_launch(mbik_plan *plan, int32_t lanes_per_skeleton);
  * the parents of segment roots).  Results do not depend on the layout. */
 int32_t mbik_plan_set_layout(mbik_plan *plan, int32_t lanes_per_skeleton, int32_t skeletons_per_block,
 		int32_t global_checkpoint_interval);
+/* Heading staging of segments with several effectors (default 1): the lanes of the
+ * segment's group split its effectors' heading builds and stage the QCP terms in LDS.  0:
+ * every lane of the group solves the segment alone from registers -- no staging LDS, so
+ * more skeletons fit per CU, at a longer step for those segments.  -1: automatic
+ * (mbik_plan_autotune times both).  Results do not depend on it. */
+int32_t mbik_plan_set_heading_staging(mbik_plan *plan, int32_t staging);
 /* Re-derives the per-skeleton setup data (bone-direction frames, Kusudama cones, tangent
  * circles and twist frames -- what mbik_plan_create computes on the host from the setup
  * pose, ManyBoneIK3D::_bone_list_changed many_bone_ik_3d.cpp:1011-1068) on the GPU for

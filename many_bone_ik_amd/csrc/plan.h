@@ -92,6 +92,11 @@ struct HostPlan {
 	// ---- launch shape ----
 	int32_t K = 4, log2K = 2, spw = 16;
 	int64_t lds_block_bytes = 0;
+	// Heading staging of multi-effector segments: split the heading work over the segment's
+	// lanes and exchange terms through LDS (true), or let every lane of the group solve the
+	// segment alone from registers (false: no staging LDS, more skeletons resident per CU,
+	// longer steps for those segments).  Not for constraint_mode (its lanes own tree ranges).
+	bool staging = true;
 	// Iteration-start globals kept in LDS only for checkpoint bones: every g_interval-th bone
 	// of a segment counted from its root (the root included) and every parent of a segment
 	// root; a bone-step rebuilds its parent's global from the nearest checkpoint above it.

@@ -1192,7 +1192,8 @@ struct mbik_plan {
 	int64_t device_bytes = 0;
 	double alg_bytes = 0;
 	double alg_flops = 0;
-	int sched_K = -1, sched_c = -1; // layout of the uploaded topology blob
+	int sched_K = -1, sched_c = -1, sched_staging = -1; // layout of the uploaded topology blob
+	int staging_override = -1;                           // mbik_plan_set_heading_staging; -1 = automatic
 	void *d_sched = nullptr; // topology blob (includes the lane schedule)
 	// scratch for mbik_solve_host
 	float *d_in = nullptr, *d_tg = nullptr, *d_out = nullptr;
@@ -1292,10 +1293,11 @@ int ensure_schedule(mbik_plan *p, int64_t nlaunch) {
 	mbik::HostPlan &h = p->host;
 	int lanes = p->lanes_override;
 	if (lanes == 0 && h.constraint_mode && p->cm_lanes > 0) lanes = p->cm_lanes;
+	h.staging = p->staging_override != 0;
 	mbik::build_schedule(h, lanes, nlaunch, p->spw_override, p->interval_override, blocks_per_cu, p, p->cu_count);
 	if (lanes == 0 && h.constraint_mode && h.K > kCmodeLanes)
 		mbik::build_schedule(h, kCmodeLanes, nlaunch, p->spw_override, p->interval_override, blocks_per_cu, p, p->cu_count);
-	if (p->sched_K == h.K && p->sched_c == h.g_interval && p->d_sched) {
+	if (p->sched_K == h.K && p->sched_c == h.g_interval && p->sched_staging == (int)h.staging && p->d_sched) {
 		p->dev.spw = h.spw;
 		return MBIK_OK;
 	}
@@ -1303,6 +1305,7 @@ int ensure_schedule(mbik_plan *p, int64_t nlaunch) {
 	if (rc) return rc;
 	p->sched_K = h.K;
 	p->sched_c = h.g_interval;
+	p->sched_staging = (int)h.staging;
 	p->dev.nrows = h.nrows;
 	p->dev.K = h.K;
 	p->dev.log2K = h.log2K;
@@ -1574,6 +1577,14 @@ int32_t mbik_plan_set_layout(mbik_plan *p, int32_t lanes, int32_t skeletons_per_
 	return MBIK_OK;
 }
 
+int32_t mbik_plan_set_heading_staging(mbik_plan *p, int32_t staging) {
+	if (!p) return fail(MBIK_EINVAL, "null plan");
+	if (staging < -1 || staging > 1) return fail(MBIK_EINVAL, "staging must be -1 (automatic), 0 or 1");
+	p->staging_override = staging;
+	p->sched_K = -1;
+	return MBIK_OK;
+}
+
 int32_t mbik_plan_rebuild_setup(mbik_plan *p, int32_t first, int32_t count, const float *setup_pose, const float *cones,
 		const float *twist, void *hip_stream) {
 	if (!p) return fail(MBIK_EINVAL, "null plan");
@@ -1711,43 +1722,51 @@ int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const flo
 	hipStream_t st = reinterpret_cast<hipStream_t>(hip_stream);
 	if (p->host.constraint_mode) return cmode_autotune(p, first, count, pose_in, targets, pose_out, st);
 	const int lanes = p->lanes_override;
+	const int staging0 = p->staging_override;
 	{
 		// A launch whose skeletons are all resident at the default layout is bound by one
 		// skeleton's dependency chain; no layout shortens that, so there is nothing to time.
 		p->spw_override = 0;
 		p->interval_override = 0;
+		p->staging_override = staging0 < 0 ? 1 : staging0;
 		int rc0 = ensure_schedule(p, count);
 		if (rc0 != MBIK_OK) return rc0;
 		if ((int64_t)blocks_per_cu(p, p->host.lds_block_bytes) * p->host.spw * p->cu_count >= count && p->host.g_interval == 1)
 			return MBIK_OK;
 	}
-	// Candidate layouts: for each checkpoint interval, the largest skeletons-per-block at each
-	// distinct residency (blocks per CU).  Every layout computes the same bits; only the time
-	// differs.
-	std::vector<std::pair<int, int>> cands; // (spw override, interval)
-	for (int c : {1, 2, 4, 1 << 20}) {
-		int last_blocks = -1;
-		for (int spw = 64; spw >= 1; spw--) {
-			mbik::build_schedule(p->host, lanes, count, spw, c, blocks_per_cu, p, p->cu_count);
-			if (p->host.spw != spw) continue; // capped by 64 / K or by LDS
-			const int blocks = blocks_per_cu(p, p->host.lds_block_bytes);
-			if (blocks != last_blocks) {
-				cands.push_back({spw, c});
-				last_blocks = blocks;
+	// Candidate layouts: for each heading-staging mode and checkpoint interval, the largest
+	// skeletons-per-block at each distinct residency (blocks per CU).  Every layout computes
+	// the same bits; only the time differs.
+	std::vector<std::tuple<int, int, int>> cands; // (spw override, interval, staging)
+	for (int stg : {1, 0}) {
+		if (staging0 >= 0 && stg != staging0) continue;
+		p->host.staging = stg != 0;
+		for (int c : {1, 2, 4, 1 << 20}) {
+			int last_blocks = -1;
+			for (int spw = 64; spw >= 1; spw--) {
+				mbik::build_schedule(p->host, lanes, count, spw, c, blocks_per_cu, p, p->cu_count);
+				if (p->host.spw != spw) continue; // capped by 64 / K or by LDS
+				const int blocks = blocks_per_cu(p, p->host.lds_block_bytes);
+				if (blocks != last_blocks) {
+					cands.push_back({spw, c, stg});
+					last_blocks = blocks;
+				}
 			}
 		}
+		if (p->host.hs_floats == 0) break; // nothing is staged: the no-staging layouts are the same
 	}
 	hipEvent_t e0, e1;
 	if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return fail(MBIK_EHIP, "hipEventCreate");
 	float best_ms = 0.0f;
-	int best_spw = 0, best_c = 0, rc = MBIK_OK;
-	std::vector<std::tuple<int, int, int>> seen; // resolved (K, spw, interval)
-	for (auto [spw, c] : cands) {
+	int best_spw = 0, best_c = 0, best_stg = 1, rc = MBIK_OK;
+	std::vector<std::tuple<int, int, int, int>> seen; // resolved (K, spw, interval, staging)
+	for (auto [spw, c, stg] : cands) {
 		p->spw_override = spw;
 		p->interval_override = c;
 		p->lanes_override = lanes;
+		p->staging_override = stg;
 		if ((rc = ensure_schedule(p, count)) != MBIK_OK) break;
-		const auto key = std::make_tuple(p->host.K, p->host.spw, p->host.g_interval);
+		const auto key = std::make_tuple(p->host.K, p->host.spw, p->host.g_interval, stg);
 		if (std::find(seen.begin(), seen.end(), key) != seen.end()) continue;
 		seen.push_back(key);
 		if ((rc = launch(p, first, count, pose_in, targets, pose_out, st, p->host.iterations, 0, p->host.NS - 1)) != MBIK_OK) break;
@@ -1766,6 +1785,7 @@ int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const flo
 			best_ms = ms;
 			best_spw = p->host.spw;
 			best_c = p->host.g_interval;
+			best_stg = stg;
 		}
 	}
 	(void)hipEventDestroy(e0);
@@ -1773,6 +1793,7 @@ int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const flo
 	if (rc != MBIK_OK) return rc;
 	p->spw_override = best_spw;
 	p->interval_override = best_c;
+	p->staging_override = best_stg;
 	return ensure_schedule(p, count);
 }
 

@@ -128,6 +128,11 @@ class Plan:
         check(self._L.mbik_plan_set_layout(self.h, int(lanes), int(skeletons_per_block),
                                            int(global_checkpoint_interval)))
 
+    def set_heading_staging(self, staging: int = -1):
+        """mbik_plan_set_heading_staging: 1 stage multi-effector segments' headings in LDS,
+        0 every lane solves such a segment alone, -1 automatic; results do not depend on it."""
+        check(self._L.mbik_plan_set_heading_staging(self.h, int(staging)))
+
     def autotune(self, pose_in_ptr: int, targets_ptr: int, pose_out_ptr: int, first: int = 0,
                  count: int | None = None, stream: int = 0):
         """mbik_plan_autotune: time candidate layouts on this batch, keep the fastest."""

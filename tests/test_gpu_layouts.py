@@ -76,3 +76,25 @@ def test_autotune_keeps_results(oracle, mbik):
     torch.cuda.synchronize()
     ref = oracle.Oracle(wl).solve(wl.pose, wl.targets, threads=8)
     assert_parity(po.cpu().numpy(), ref, "C2 after autotune")
+
+
+@pytest.mark.parametrize("cfg,n", [(2, 48), (3, 48), (4, 16), (5, 6)])
+@pytest.mark.parametrize("stab", [0, 2])
+@pytest.mark.parametrize("lanes", [0, 16])
+def test_unstaged_headings_bitwise_vs_oracle(oracle, mbik, cfg, n, stab, lanes):
+    """mbik_plan_set_heading_staging(0): every lane of a multi-effector segment's group solves
+    the segment alone (no LDS staging); still bitwise equal to the oracle."""
+    wl = W.generate(cfg, n, first=9000)
+    ref = oracle.Oracle(wl, stabilization_passes=stab).solve(wl.pose, wl.targets, threads=8)
+    plan = Plan.from_workload(wl, stabilization_passes=stab)
+    plan.set_layout(lanes, 0, 0)
+    plan.set_heading_staging(0)
+    got = plan.solve_host(wl.pose, wl.targets)
+    assert_parity(got, ref, f"C{cfg} unstaged lanes={lanes} stab={stab}")
+
+
+def test_staging_argument_check(mbik):
+    plan = Plan.from_workload(W.generate(3, 2))
+    with pytest.raises(_lib.MbikError):
+        plan.set_heading_staging(2)
+    plan.set_heading_staging(-1)
