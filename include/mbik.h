@@ -127,6 +127,11 @@ int32_t mbik_plan_set_layout(mbik_plan *plan, int32_t lanes_per_skeleton, int32_
  * more skeletons fit per CU, at a longer step for those segments.  -1: automatic
  * (mbik_plan_autotune times both).  Results do not depend on it. */
 int32_t mbik_plan_set_heading_staging(mbik_plan *plan, int32_t staging);
+/* Where the solve keeps the bone local transforms during a launch: 0 (default) LDS, 1 a
+ * per-skeleton area in device memory (L2-resident; half the LDS of a long-chain skeleton,
+ * so more skeletons resident per CU), -1 automatic (mbik_plan_autotune times both).
+ * Results do not depend on it. */
+int32_t mbik_plan_set_locals_placement(mbik_plan *plan, int32_t placement);
 /* Re-derives the per-skeleton setup data (bone-direction frames, Kusudama cones, tangent
  * circles and twist frames -- what mbik_plan_create computes on the host from the setup
  * pose, ManyBoneIK3D::_bone_list_changed many_bone_ik_3d.cpp:1011-1068) on the GPU for

@@ -431,7 +431,7 @@ std::string build_skeletons(HostPlan &p, int32_t n, const float *setup_pose, con
 // Launch shape + sibling-level schedule
 // ---------------------------------------------------------------------------------------
 int32_t lds_floats_per_skeleton(const HostPlan &p) {
-	return p.B * 12 + p.n_gck * 12 + p.P * 25 + p.hs_floats + (p.stabilization_passes > 0 ? p.P * 10 : 0);
+	return (p.locals_hbm ? 0 : p.B * 12) + p.n_gck * 12 + p.P * 25 + p.hs_floats + (p.stabilization_passes > 0 ? p.P * 10 : 0);
 }
 
 // Upper bound of the LDS bytes taken by the topology blob (solve.hip: upload_topology).

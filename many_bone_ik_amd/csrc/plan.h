@@ -97,6 +97,10 @@ struct HostPlan {
 	// segment alone from registers (false: no staging LDS, more skeletons resident per CU,
 	// longer steps for those segments).  Not for constraint_mode (its lanes own tree ranges).
 	bool staging = true;
+	// Bone local transforms (the solve state L) in LDS (false) or in a per-skeleton HBM area
+	// (true): half the LDS of a long-chain skeleton, so twice the skeletons resident per CU,
+	// for L2 instead of LDS latency on those accesses.
+	bool locals_hbm = false;
 	// Iteration-start globals kept in LDS only for checkpoint bones: every g_interval-th bone
 	// of a segment counted from its root (the root included) and every parent of a segment
 	// root; a bone-step rebuilds its parent's global from the nearest checkpoint above it.

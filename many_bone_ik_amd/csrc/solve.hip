@@ -85,6 +85,8 @@ struct DevPlan {
 	// mbik_solve_checked: per-skeleton flag, 1 when any bone's solved basis was non-finite and
 	// was written as the identity rotation (ik_bone_3d.cpp:174-176); null otherwise.
 	unsigned char *nonfinite = nullptr;
+	// locals_hbm layouts: the bone local transforms of skeleton s at Lg + s * 12 * B
+	float *Lg = nullptr;
 };
 
 // ------------------------------------------------------------------------------------
@@ -989,7 +991,7 @@ __device__ __forceinline__ void write_nonfinite(const DevPlan &t, bool valid, bo
 #define MBIK_WAVES_PER_EU 1
 #endif
 // The solve of one block (blk = the plan-local block index after the XCD remap).
-template <bool STAB>
+template <bool STAB, bool LH>
 __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int count, const float *__restrict__ pose_in,
 		const float *__restrict__ targets, float *__restrict__ pose_out, int iterations, int seg_lo, int seg_hi) {
 	extern __shared__ float4 lds4[];
@@ -1025,8 +1027,9 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 	const bool valid = g < t.spw && local < count;
 	const size_t s = (size_t)first + (size_t)(valid ? local : 0);
 	const int B = t.B, P = t.P, K = t.K;
-	float *L = lds + (size_t)g * t.lds_stride;
-	float *G = L + 12 * B;
+	// LH: the locals live in HBM (L2-resident per launch), the rest of the state in LDS
+	float *L = LH ? t.Lg + s * 12 * (size_t)B : lds + (size_t)g * t.lds_stride;
+	float *G = LH ? lds + (size_t)g * t.lds_stride : L + 12 * B;
 	float *TG = G + 12 * t.n_gck;
 	float *ST = TG + 12 * P;
 	float *HS = ST + 12 * P;                        // staged headings (t.seg_hbase), 16-B aligned
@@ -1106,10 +1109,10 @@ __device__ __forceinline__ int xcd_block() {
 #endif
 }
 
-template <bool STAB>
+template <bool STAB, bool LH>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MBIK_WAVES_PER_EU, MBIK_WAVES_PER_EU))) void mbik_solve_kernel(DevPlan t, int first, int count, const float *__restrict__ pose_in,
 		const float *__restrict__ targets, float *__restrict__ pose_out, int iterations, int seg_lo, int seg_hi) {
-	solve_block<STAB>(t, xcd_block(), first, count, pose_in, targets, pose_out, iterations, seg_lo, seg_hi);
+	solve_block<STAB, LH>(t, xcd_block(), first, count, pose_in, targets, pose_out, iterations, seg_lo, seg_hi);
 }
 
 // A heterogeneous batch (mbik_group_solve): several plans -- distinct rigs -- in one launch.
@@ -1134,7 +1137,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MBIK_WAVES_P
 	}
 	DevPlan t = plans[lo];
 	const GroupEntry e = entries[lo];
-	solve_block<STAB>(t, gb - e.block_off, e.first, e.count, e.pose_in, e.targets, e.pose_out, e.iterations, 0, t.NS - 1);
+	solve_block<STAB, false>(t, gb - e.block_off, e.first, e.count, e.pose_in, e.targets, e.pose_out, e.iterations, 0, t.NS - 1);
 }
 
 #include "cmode.h"
@@ -1194,6 +1197,9 @@ struct mbik_plan {
 	double alg_flops = 0;
 	int sched_K = -1, sched_c = -1, sched_staging = -1; // layout of the uploaded topology blob
 	int staging_override = -1;                           // mbik_plan_set_heading_staging; -1 = automatic
+	int locals_override = -1;                            // mbik_plan_set_locals_placement; -1 = automatic
+	int sched_locals = -1;
+	float *d_locals = nullptr;                           // [N][B][12] for locals_hbm layouts
 	void *d_sched = nullptr; // topology blob (includes the lane schedule)
 	// scratch for mbik_solve_host
 	float *d_in = nullptr, *d_tg = nullptr, *d_out = nullptr;
@@ -1268,17 +1274,26 @@ int upload_topology(mbik_plan *p) {
 	return MBIK_OK;
 }
 
+using SolveKernel = void (*)(DevPlan, int, int, const float *, const float *, float *, int, int, int);
+// The solve kernel instantiation of a plan's current layout (stabilization x locals placement).
+SolveKernel solve_kernel_for(const mbik::HostPlan &h) {
+	static std::once_flag once;
+	std::call_once(once, [] {
+		for (const void *k : {(const void *)mbik_solve_kernel<false, false>, (const void *)mbik_solve_kernel<true, false>,
+					 (const void *)mbik_solve_kernel<false, true>, (const void *)mbik_solve_kernel<true, true>})
+			(void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+	});
+	const bool st = h.stabilization_passes > 0;
+	if (h.locals_hbm) return st ? mbik_solve_kernel<true, true> : mbik_solve_kernel<false, true>;
+	return st ? mbik_solve_kernel<true, false> : mbik_solve_kernel<false, false>;
+}
+
 // Resident one-wave blocks per CU for a block's LDS size, from the runtime's occupancy
 // query on the kernel instantiation the plan launches (LDS granularity and registers).
 int blocks_per_cu(void *ctx, int64_t lds_bytes) {
 	const mbik_plan *p = static_cast<const mbik_plan *>(ctx);
-	static std::once_flag once;
-	std::call_once(once, [] {
-		(void)hipFuncSetAttribute((const void *)mbik_solve_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-		(void)hipFuncSetAttribute((const void *)mbik_solve_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-	});
 	int n = 0;
-	const void *k = p->host.stabilization_passes > 0 ? (const void *)mbik_solve_kernel<true> : (const void *)mbik_solve_kernel<false>;
+	const void *k = (const void *)solve_kernel_for(p->host);
 	if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, 64, (size_t)lds_bytes) != hipSuccess || n <= 0)
 		return (int)(160 * 1024 / std::max<int64_t>(1, lds_bytes));
 	return n;
@@ -1294,10 +1309,19 @@ int ensure_schedule(mbik_plan *p, int64_t nlaunch) {
 	int lanes = p->lanes_override;
 	if (lanes == 0 && h.constraint_mode && p->cm_lanes > 0) lanes = p->cm_lanes;
 	h.staging = p->staging_override != 0;
+	h.locals_hbm = p->locals_override == 1 && !h.constraint_mode;
+	if (h.locals_hbm && !p->d_locals) {
+		const size_t bytes = (size_t)h.N * h.B * 12 * sizeof(float);
+		if (hipMalloc(&p->d_locals, bytes) != hipSuccess) return fail(MBIK_ENOMEM, "hipMalloc locals");
+		p->allocs.push_back(p->d_locals);
+		p->device_bytes += (int64_t)bytes;
+		p->dev.Lg = p->d_locals;
+	}
 	mbik::build_schedule(h, lanes, nlaunch, p->spw_override, p->interval_override, blocks_per_cu, p, p->cu_count);
 	if (lanes == 0 && h.constraint_mode && h.K > kCmodeLanes)
 		mbik::build_schedule(h, kCmodeLanes, nlaunch, p->spw_override, p->interval_override, blocks_per_cu, p, p->cu_count);
-	if (p->sched_K == h.K && p->sched_c == h.g_interval && p->sched_staging == (int)h.staging && p->d_sched) {
+	if (p->sched_K == h.K && p->sched_c == h.g_interval && p->sched_staging == (int)h.staging &&
+			p->sched_locals == (int)h.locals_hbm && p->d_sched) {
 		p->dev.spw = h.spw;
 		return MBIK_OK;
 	}
@@ -1306,6 +1330,7 @@ int ensure_schedule(mbik_plan *p, int64_t nlaunch) {
 	p->sched_K = h.K;
 	p->sched_c = h.g_interval;
 	p->sched_staging = (int)h.staging;
+	p->sched_locals = (int)h.locals_hbm;
 	p->dev.nrows = h.nrows;
 	p->dev.K = h.K;
 	p->dev.log2K = h.log2K;
@@ -1404,13 +1429,8 @@ int launch(mbik_plan *p, int first, int count, const float *pose_in, const float
 	lds += ((size_t)p->dev.B * 9 + p->dev.NC * p->dev.cf_stride + 2 * p->dev.NC * p->dev.cd_stride + 2) * sizeof(float);
 #endif
 	if (lds > 160 * 1024) return fail(MBIK_EUNSUPPORTED, "skeleton too large for LDS at this lane count");
-	static std::once_flag once;
-	std::call_once(once, [] {
-		(void)hipFuncSetAttribute((const void *)mbik_solve_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-		(void)hipFuncSetAttribute((const void *)mbik_solve_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-	});
 	unsigned blocks = (unsigned)((count + h.spw - 1) / h.spw);
-	auto kern = h.stabilization_passes > 0 ? mbik_solve_kernel<true> : mbik_solve_kernel<false>;
+	auto kern = solve_kernel_for(h);
 	hipLaunchKernelGGL(kern, dim3(blocks), dim3(64), lds, stream, p->dev, first, count, pose_in, targets, pose_out,
 			iterations, seg_lo, seg_hi);
 	hipError_t e = hipGetLastError();
@@ -1577,6 +1597,14 @@ int32_t mbik_plan_set_layout(mbik_plan *p, int32_t lanes, int32_t skeletons_per_
 	return MBIK_OK;
 }
 
+int32_t mbik_plan_set_locals_placement(mbik_plan *p, int32_t placement) {
+	if (!p) return fail(MBIK_EINVAL, "null plan");
+	if (placement < -1 || placement > 1) return fail(MBIK_EINVAL, "placement must be -1 (automatic), 0 (LDS) or 1 (HBM)");
+	p->locals_override = placement;
+	p->sched_K = -1;
+	return MBIK_OK;
+}
+
 int32_t mbik_plan_set_heading_staging(mbik_plan *p, int32_t staging) {
 	if (!p) return fail(MBIK_EINVAL, "null plan");
 	if (staging < -1 || staging > 1) return fail(MBIK_EINVAL, "staging must be -1 (automatic), 0 or 1");
@@ -1723,12 +1751,14 @@ int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const flo
 	if (p->host.constraint_mode) return cmode_autotune(p, first, count, pose_in, targets, pose_out, st);
 	const int lanes = p->lanes_override;
 	const int staging0 = p->staging_override;
+	const int locals0 = p->locals_override;
 	{
 		// A launch whose skeletons are all resident at the default layout is bound by one
 		// skeleton's dependency chain; no layout shortens that, so there is nothing to time.
 		p->spw_override = 0;
 		p->interval_override = 0;
 		p->staging_override = staging0 < 0 ? 1 : staging0;
+		p->locals_override = locals0 < 0 ? 0 : locals0;
 		int rc0 = ensure_schedule(p, count);
 		if (rc0 != MBIK_OK) return rc0;
 		if ((int64_t)blocks_per_cu(p, p->host.lds_block_bytes) * p->host.spw * p->cu_count >= count && p->host.g_interval == 1)
@@ -1737,36 +1767,41 @@ int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const flo
 	// Candidate layouts: for each heading-staging mode and checkpoint interval, the largest
 	// skeletons-per-block at each distinct residency (blocks per CU).  Every layout computes
 	// the same bits; only the time differs.
-	std::vector<std::tuple<int, int, int>> cands; // (spw override, interval, staging)
-	for (int stg : {1, 0}) {
-		if (staging0 >= 0 && stg != staging0) continue;
-		p->host.staging = stg != 0;
-		for (int c : {1, 2, 4, 1 << 20}) {
-			int last_blocks = -1;
-			for (int spw = 64; spw >= 1; spw--) {
-				mbik::build_schedule(p->host, lanes, count, spw, c, blocks_per_cu, p, p->cu_count);
-				if (p->host.spw != spw) continue; // capped by 64 / K or by LDS
-				const int blocks = blocks_per_cu(p, p->host.lds_block_bytes);
-				if (blocks != last_blocks) {
-					cands.push_back({spw, c, stg});
-					last_blocks = blocks;
+	std::vector<std::tuple<int, int, int, int>> cands; // (spw override, interval, staging, locals in HBM)
+	for (int lh : {0, 1}) {
+		if (locals0 >= 0 && lh != locals0) continue;
+		p->host.locals_hbm = lh != 0;
+		for (int stg : {1, 0}) {
+			if (staging0 >= 0 && stg != staging0) continue;
+			p->host.staging = stg != 0;
+			for (int c : {1, 2, 4, 1 << 20}) {
+				int last_blocks = -1;
+				for (int spw = 64; spw >= 1; spw--) {
+					mbik::build_schedule(p->host, lanes, count, spw, c, blocks_per_cu, p, p->cu_count);
+					if (p->host.spw != spw) continue; // capped by 64 / K or by LDS
+					const int blocks = blocks_per_cu(p, p->host.lds_block_bytes);
+					if (blocks != last_blocks) {
+						cands.push_back({spw, c, stg, lh});
+						last_blocks = blocks;
+					}
 				}
 			}
+			if (p->host.hs_floats == 0) break; // nothing is staged: the no-staging layouts are the same
 		}
-		if (p->host.hs_floats == 0) break; // nothing is staged: the no-staging layouts are the same
 	}
 	hipEvent_t e0, e1;
 	if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return fail(MBIK_EHIP, "hipEventCreate");
 	float best_ms = 0.0f;
-	int best_spw = 0, best_c = 0, best_stg = 1, rc = MBIK_OK;
-	std::vector<std::tuple<int, int, int, int>> seen; // resolved (K, spw, interval, staging)
-	for (auto [spw, c, stg] : cands) {
+	int best_spw = 0, best_c = 0, best_stg = 1, best_lh = 0, rc = MBIK_OK;
+	std::vector<std::tuple<int, int, int, int, int>> seen; // resolved (K, spw, interval, staging, locals)
+	for (auto [spw, c, stg, lh] : cands) {
 		p->spw_override = spw;
 		p->interval_override = c;
 		p->lanes_override = lanes;
 		p->staging_override = stg;
+		p->locals_override = lh;
 		if ((rc = ensure_schedule(p, count)) != MBIK_OK) break;
-		const auto key = std::make_tuple(p->host.K, p->host.spw, p->host.g_interval, stg);
+		const auto key = std::make_tuple(p->host.K, p->host.spw, p->host.g_interval, stg, lh);
 		if (std::find(seen.begin(), seen.end(), key) != seen.end()) continue;
 		seen.push_back(key);
 		if ((rc = launch(p, first, count, pose_in, targets, pose_out, st, p->host.iterations, 0, p->host.NS - 1)) != MBIK_OK) break;
@@ -1786,6 +1821,7 @@ int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const flo
 			best_spw = p->host.spw;
 			best_c = p->host.g_interval;
 			best_stg = stg;
+			best_lh = lh;
 		}
 	}
 	(void)hipEventDestroy(e0);
@@ -1794,6 +1830,7 @@ int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const flo
 	p->spw_override = best_spw;
 	p->interval_override = best_c;
 	p->staging_override = best_stg;
+	p->locals_override = best_lh;
 	return ensure_schedule(p, count);
 }
 
@@ -1930,14 +1967,15 @@ int32_t mbik_group_solve(mbik_group *g, const int32_t *first, const int32_t *cou
 		if (f < 0 || c < 0 || (int64_t)f + c > p->host.N) return fail(MBIK_EINVAL, "skeleton range out of plan");
 		if (c == 0) continue;
 		if (!pose_in[i] || !pose_out[i] || (p->host.P > 0 && !targets[i])) return fail(MBIK_EINVAL, "null buffer");
-		if (p->host.constraint_mode || p->host.P == 0) {
-			// constraint_mode plans have their own kernel; pinless plans only copy
-			int rc = launch(p, f, c, pose_in[i], targets[i], pose_out[i], stream, p->host.iterations, 0, p->host.NS - 1);
+		int rc = p->host.P > 0 ? ensure_schedule(p, c) : MBIK_OK;
+		if (rc) return rc;
+		if (p->host.constraint_mode || p->host.P == 0 || p->host.locals_hbm) {
+			// constraint_mode plans have their own kernel, so do plans laid out with their
+			// locals in HBM; pinless plans only copy
+			rc = launch(p, f, c, pose_in[i], targets[i], pose_out[i], stream, p->host.iterations, 0, p->host.NS - 1);
 			if (rc) return rc;
 			continue;
 		}
-		int rc = ensure_schedule(p, c);
-		if (rc) return rc;
 		const mbik::HostPlan &h = p->host;
 		const size_t l = ((size_t)h.spw * p->dev.lds_stride + p->dev.topo_words) * sizeof(float);
 		if (l > 160 * 1024) return fail(MBIK_EUNSUPPORTED, "skeleton too large for LDS at this lane count");

@@ -133,6 +133,10 @@ class Plan:
         0 every lane solves such a segment alone, -1 automatic; results do not depend on it."""
         check(self._L.mbik_plan_set_heading_staging(self.h, int(staging)))
 
+    def set_locals_placement(self, placement: int = -1):
+        """mbik_plan_set_locals_placement: 0 bone locals in LDS, 1 in device memory, -1 automatic."""
+        check(self._L.mbik_plan_set_locals_placement(self.h, int(placement)))
+
     def autotune(self, pose_in_ptr: int, targets_ptr: int, pose_out_ptr: int, first: int = 0,
                  count: int | None = None, stream: int = 0):
         """mbik_plan_autotune: time candidate layouts on this batch, keep the fastest."""

@@ -98,3 +98,49 @@ def test_staging_argument_check(mbik):
     with pytest.raises(_lib.MbikError):
         plan.set_heading_staging(2)
     plan.set_heading_staging(-1)
+
+
+@pytest.mark.parametrize("cfg,n", [(1, 8), (2, 48), (3, 48), (4, 16), (5, 6)])
+@pytest.mark.parametrize("staging", [1, 0])
+@pytest.mark.parametrize("stab", [0, 2])
+def test_locals_in_hbm_bitwise_vs_oracle(oracle, mbik, cfg, n, staging, stab):
+    """mbik_plan_set_locals_placement(1): the bone locals live in device memory during the
+    launch (sibling lanes exchange them through L2 across the row barriers); bitwise equal."""
+    wl = W.generate(cfg, n, first=12000)
+    ref = oracle.Oracle(wl, stabilization_passes=stab).solve(wl.pose, wl.targets, threads=8)
+    plan = Plan.from_workload(wl, stabilization_passes=stab)
+    plan.set_locals_placement(1)
+    plan.set_heading_staging(staging)
+    got = plan.solve_host(wl.pose, wl.targets)
+    assert_parity(got, ref, f"C{cfg} locals in HBM staging={staging} stab={stab}")
+    plan.set_locals_placement(0)                          # back to LDS: same bits
+    assert_parity(plan.solve_host(wl.pose, wl.targets), ref, f"C{cfg} locals back in LDS")
+
+
+def test_locals_in_hbm_subrange_and_group(oracle, mbik):
+    """A subrange launch indexes the HBM locals by absolute skeleton; a group with such a plan
+    launches it on its own and the results stay exact."""
+    from many_bone_ik_amd.solver import Group
+    wl = W.generate(2, 40, first=300)
+    ref = oracle.Oracle(wl).solve(wl.pose, wl.targets, threads=8)
+    plan = Plan.from_workload(wl)
+    plan.set_locals_placement(1)
+    import torch
+    dev = torch.device("cuda", 0)
+    pi = torch.from_numpy(wl.pose).to(dev)
+    tg = torch.from_numpy(wl.targets).to(dev)
+    po = torch.zeros_like(pi)
+    plan.solve(pi[10].data_ptr(), tg[10].data_ptr(), po[10].data_ptr(), 10, 20)
+    torch.cuda.synchronize()
+    assert_parity(po[10:30].cpu().numpy(), ref[10:30], "HBM locals subrange")
+    wl3 = W.generate(3, 24, first=50)
+    ref3 = oracle.Oracle(wl3).solve(wl3.pose, wl3.targets, threads=8)
+    plan3 = Plan.from_workload(wl3)
+    grp = Group([plan, plan3])
+    pi3 = torch.from_numpy(wl3.pose).to(dev)
+    tg3 = torch.from_numpy(wl3.targets).to(dev)
+    po1, po3 = torch.empty_like(pi), torch.empty_like(pi3)
+    grp.solve([pi.data_ptr(), pi3.data_ptr()], [tg.data_ptr(), tg3.data_ptr()], [po1.data_ptr(), po3.data_ptr()])
+    torch.cuda.synchronize()
+    assert_parity(po1.cpu().numpy(), ref, "group: HBM-locals plan")
+    assert_parity(po3.cpu().numpy(), ref3, "group: LDS plan")
