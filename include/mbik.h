@@ -127,10 +127,11 @@ int32_t mbik_plan_set_layout(mbik_plan *plan, int32_t lanes_per_skeleton, int32_
  * more skeletons fit per CU, at a longer step for those segments.  -1: automatic
  * (mbik_plan_autotune times both).  Results do not depend on it. */
 int32_t mbik_plan_set_heading_staging(mbik_plan *plan, int32_t staging);
-/* Where the solve keeps the bone local transforms during a launch: 0 (default) LDS, 1 a
- * per-skeleton area in device memory (L2-resident; half the LDS of a long-chain skeleton,
- * so more skeletons resident per CU), -1 automatic (mbik_plan_autotune times both).
- * Results do not depend on it. */
+/* Where the solve keeps its per-skeleton state during a launch: 0 (default) all in LDS;
+ * 1 the bone local transforms in a per-skeleton device-memory area (L2-resident; about half
+ * the LDS of a long-chain skeleton), the rest in LDS; 2 all of it in device memory (LDS holds
+ * only the block's topology copy).  Less LDS per skeleton, more skeletons resident per CU.
+ * -1: automatic (mbik_plan_autotune times each).  Results do not depend on it. */
 int32_t mbik_plan_set_locals_placement(mbik_plan *plan, int32_t placement);
 /* Re-derives the per-skeleton setup data (bone-direction frames, Kusudama cones, tangent
  * circles and twist frames -- what mbik_plan_create computes on the host from the setup

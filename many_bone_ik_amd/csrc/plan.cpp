@@ -431,7 +431,12 @@ std::string build_skeletons(HostPlan &p, int32_t n, const float *setup_pose, con
 // Launch shape + sibling-level schedule
 // ---------------------------------------------------------------------------------------
 int32_t lds_floats_per_skeleton(const HostPlan &p) {
-	return (p.locals_hbm ? 0 : p.B * 12) + p.n_gck * 12 + p.P * 25 + p.hs_floats + (p.stabilization_passes > 0 ? p.P * 10 : 0);
+	const int32_t all = state_floats_per_skeleton(p);
+	return p.state_hbm == 2 ? 0 : (p.state_hbm == 1 ? all - p.B * 12 : all);
+}
+// The whole per-skeleton state: L, checkpoint globals, targets, stale caches, staging, stabilization.
+int32_t state_floats_per_skeleton(const HostPlan &p) {
+	return p.B * 12 + p.n_gck * 12 + p.P * 25 + p.hs_floats + (p.stabilization_passes > 0 ? p.P * 10 : 0);
 }
 
 // Upper bound of the LDS bytes taken by the topology blob (solve.hip: upload_topology).

@@ -97,10 +97,11 @@ struct HostPlan {
 	// segment alone from registers (false: no staging LDS, more skeletons resident per CU,
 	// longer steps for those segments).  Not for constraint_mode (its lanes own tree ranges).
 	bool staging = true;
-	// Bone local transforms (the solve state L) in LDS (false) or in a per-skeleton HBM area
-	// (true): half the LDS of a long-chain skeleton, so twice the skeletons resident per CU,
-	// for L2 instead of LDS latency on those accesses.
-	bool locals_hbm = false;
+	// Where the per-skeleton solve state lives during a launch: 0 all of it in LDS; 1 the
+	// bone local transforms L in a per-skeleton device-memory area (L2-resident), the rest in
+	// LDS; 2 all of it in device memory (LDS holds only the block's topology copy).  Less LDS
+	// per skeleton means more skeletons resident per CU, for L2 instead of LDS latency.
+	int32_t state_hbm = 0;
 	// Iteration-start globals kept in LDS only for checkpoint bones: every g_interval-th bone
 	// of a segment counted from its root (the root included) and every parent of a segment
 	// root; a bone-step rebuilds its parent's global from the nearest checkpoint above it.
@@ -140,6 +141,7 @@ void build_schedule(HostPlan &plan, int32_t lanes_per_skeleton, int64_t skeleton
 // stabilization the pre-loop target
 // origins (3 per pin) and the manual-MSD terms (7 per pin).
 int32_t lds_floats_per_skeleton(const HostPlan &plan);
+int32_t state_floats_per_skeleton(const HostPlan &plan);
 int64_t topology_bytes(const HostPlan &plan);
 
 } // namespace mbik

@@ -85,8 +85,10 @@ struct DevPlan {
 	// mbik_solve_checked: per-skeleton flag, 1 when any bone's solved basis was non-finite and
 	// was written as the identity rotation (ik_bone_3d.cpp:174-176); null otherwise.
 	unsigned char *nonfinite = nullptr;
-	// locals_hbm layouts: the bone local transforms of skeleton s at Lg + s * 12 * B
-	float *Lg = nullptr;
+	// state_hbm 1: the bone locals of skeleton s at Lg + s * 12 * B; state_hbm 2: its whole
+	// state at Sg + s * state_stride (the LDS layout of one skeleton)
+	float *Lg = nullptr, *Sg = nullptr;
+	int state_stride = 0;
 };
 
 // ------------------------------------------------------------------------------------
@@ -991,7 +993,7 @@ __device__ __forceinline__ void write_nonfinite(const DevPlan &t, bool valid, bo
 #define MBIK_WAVES_PER_EU 1
 #endif
 // The solve of one block (blk = the plan-local block index after the XCD remap).
-template <bool STAB, bool LH>
+template <bool STAB, int PL>
 __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int count, const float *__restrict__ pose_in,
 		const float *__restrict__ targets, float *__restrict__ pose_out, int iterations, int seg_lo, int seg_hi) {
 	extern __shared__ float4 lds4[];
@@ -1027,9 +1029,19 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 	const bool valid = g < t.spw && local < count;
 	const size_t s = (size_t)first + (size_t)(valid ? local : 0);
 	const int B = t.B, P = t.P, K = t.K;
-	// LH: the locals live in HBM (L2-resident per launch), the rest of the state in LDS
-	float *L = LH ? t.Lg + s * 12 * (size_t)B : lds + (size_t)g * t.lds_stride;
-	float *G = LH ? lds + (size_t)g * t.lds_stride : L + 12 * B;
+	// PL (HostPlan::state_hbm): 0 the state in LDS; 1 the locals in device memory (L2-resident
+	// during the launch), the rest in LDS; 2 all of it in device memory
+	float *L, *G;
+	if constexpr (PL == 2) {
+		L = t.Sg + s * (size_t)t.state_stride;
+		G = L + 12 * B;
+	} else if constexpr (PL == 1) {
+		L = t.Lg + s * 12 * (size_t)B;
+		G = lds + (size_t)g * t.lds_stride;
+	} else {
+		L = lds + (size_t)g * t.lds_stride;
+		G = L + 12 * B;
+	}
 	float *TG = G + 12 * t.n_gck;
 	float *ST = TG + 12 * P;
 	float *HS = ST + 12 * P;                        // staged headings (t.seg_hbase), 16-B aligned
@@ -1109,10 +1121,10 @@ __device__ __forceinline__ int xcd_block() {
 #endif
 }
 
-template <bool STAB, bool LH>
+template <bool STAB, int PL>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MBIK_WAVES_PER_EU, MBIK_WAVES_PER_EU))) void mbik_solve_kernel(DevPlan t, int first, int count, const float *__restrict__ pose_in,
 		const float *__restrict__ targets, float *__restrict__ pose_out, int iterations, int seg_lo, int seg_hi) {
-	solve_block<STAB, LH>(t, xcd_block(), first, count, pose_in, targets, pose_out, iterations, seg_lo, seg_hi);
+	solve_block<STAB, PL>(t, xcd_block(), first, count, pose_in, targets, pose_out, iterations, seg_lo, seg_hi);
 }
 
 // A heterogeneous batch (mbik_group_solve): several plans -- distinct rigs -- in one launch.
@@ -1137,7 +1149,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MBIK_WAVES_P
 	}
 	DevPlan t = plans[lo];
 	const GroupEntry e = entries[lo];
-	solve_block<STAB, false>(t, gb - e.block_off, e.first, e.count, e.pose_in, e.targets, e.pose_out, e.iterations, 0, t.NS - 1);
+	solve_block<STAB, 0>(t, gb - e.block_off, e.first, e.count, e.pose_in, e.targets, e.pose_out, e.iterations, 0, t.NS - 1);
 }
 
 #include "cmode.h"
@@ -1199,7 +1211,9 @@ struct mbik_plan {
 	int staging_override = -1;                           // mbik_plan_set_heading_staging; -1 = automatic
 	int locals_override = -1;                            // mbik_plan_set_locals_placement; -1 = automatic
 	int sched_locals = -1;
-	float *d_locals = nullptr;                           // [N][B][12] for locals_hbm layouts
+	float *d_locals = nullptr;                           // [N][B][12] for state_hbm 1
+	float *d_state = nullptr;                            // [N][state stride] for state_hbm 2
+	size_t d_state_floats = 0;
 	void *d_sched = nullptr; // topology blob (includes the lane schedule)
 	// scratch for mbik_solve_host
 	float *d_in = nullptr, *d_tg = nullptr, *d_out = nullptr;
@@ -1277,15 +1291,14 @@ int upload_topology(mbik_plan *p) {
 using SolveKernel = void (*)(DevPlan, int, int, const float *, const float *, float *, int, int, int);
 // The solve kernel instantiation of a plan's current layout (stabilization x locals placement).
 SolveKernel solve_kernel_for(const mbik::HostPlan &h) {
+	static const SolveKernel ks[2][3] = {{mbik_solve_kernel<false, 0>, mbik_solve_kernel<false, 1>, mbik_solve_kernel<false, 2>},
+			{mbik_solve_kernel<true, 0>, mbik_solve_kernel<true, 1>, mbik_solve_kernel<true, 2>}};
 	static std::once_flag once;
 	std::call_once(once, [] {
-		for (const void *k : {(const void *)mbik_solve_kernel<false, false>, (const void *)mbik_solve_kernel<true, false>,
-					 (const void *)mbik_solve_kernel<false, true>, (const void *)mbik_solve_kernel<true, true>})
-			(void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+		for (auto &row : ks)
+			for (SolveKernel k : row) (void)hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 	});
-	const bool st = h.stabilization_passes > 0;
-	if (h.locals_hbm) return st ? mbik_solve_kernel<true, true> : mbik_solve_kernel<false, true>;
-	return st ? mbik_solve_kernel<true, false> : mbik_solve_kernel<false, false>;
+	return ks[h.stabilization_passes > 0 ? 1 : 0][std::min(2, std::max(0, (int)h.state_hbm))];
 }
 
 // Resident one-wave blocks per CU for a block's LDS size, from the runtime's occupancy
@@ -1309,8 +1322,8 @@ int ensure_schedule(mbik_plan *p, int64_t nlaunch) {
 	int lanes = p->lanes_override;
 	if (lanes == 0 && h.constraint_mode && p->cm_lanes > 0) lanes = p->cm_lanes;
 	h.staging = p->staging_override != 0;
-	h.locals_hbm = p->locals_override == 1 && !h.constraint_mode;
-	if (h.locals_hbm && !p->d_locals) {
+	h.state_hbm = h.constraint_mode ? 0 : std::max(0, p->locals_override);
+	if (h.state_hbm == 1 && !p->d_locals) {
 		const size_t bytes = (size_t)h.N * h.B * 12 * sizeof(float);
 		if (hipMalloc(&p->d_locals, bytes) != hipSuccess) return fail(MBIK_ENOMEM, "hipMalloc locals");
 		p->allocs.push_back(p->d_locals);
@@ -1320,8 +1333,28 @@ int ensure_schedule(mbik_plan *p, int64_t nlaunch) {
 	mbik::build_schedule(h, lanes, nlaunch, p->spw_override, p->interval_override, blocks_per_cu, p, p->cu_count);
 	if (lanes == 0 && h.constraint_mode && h.K > kCmodeLanes)
 		mbik::build_schedule(h, kCmodeLanes, nlaunch, p->spw_override, p->interval_override, blocks_per_cu, p, p->cu_count);
+	if (h.state_hbm == 2) {
+		// the whole state in device memory: one skeleton's LDS layout per skeleton
+		const int stride = (mbik::state_floats_per_skeleton(h) + 3) & ~3;
+		const size_t need = (size_t)h.N * stride;
+		if (need > p->d_state_floats) {
+			void *a = nullptr;
+			if (hipMalloc(&a, need * sizeof(float)) != hipSuccess) return fail(MBIK_ENOMEM, "hipMalloc state");
+			if (p->d_state) {
+				(void)hipFree(p->d_state);
+				p->allocs.erase(std::remove(p->allocs.begin(), p->allocs.end(), (void *)p->d_state), p->allocs.end());
+				p->device_bytes -= (int64_t)(p->d_state_floats * sizeof(float));
+			}
+			p->d_state = static_cast<float *>(a);
+			p->d_state_floats = need;
+			p->allocs.push_back(a);
+			p->device_bytes += (int64_t)(need * sizeof(float));
+		}
+		p->dev.Sg = p->d_state;
+		p->dev.state_stride = stride;
+	}
 	if (p->sched_K == h.K && p->sched_c == h.g_interval && p->sched_staging == (int)h.staging &&
-			p->sched_locals == (int)h.locals_hbm && p->d_sched) {
+			p->sched_locals == h.state_hbm && p->d_sched) {
 		p->dev.spw = h.spw;
 		return MBIK_OK;
 	}
@@ -1330,7 +1363,7 @@ int ensure_schedule(mbik_plan *p, int64_t nlaunch) {
 	p->sched_K = h.K;
 	p->sched_c = h.g_interval;
 	p->sched_staging = (int)h.staging;
-	p->sched_locals = (int)h.locals_hbm;
+	p->sched_locals = h.state_hbm;
 	p->dev.nrows = h.nrows;
 	p->dev.K = h.K;
 	p->dev.log2K = h.log2K;
@@ -1599,7 +1632,8 @@ int32_t mbik_plan_set_layout(mbik_plan *p, int32_t lanes, int32_t skeletons_per_
 
 int32_t mbik_plan_set_locals_placement(mbik_plan *p, int32_t placement) {
 	if (!p) return fail(MBIK_EINVAL, "null plan");
-	if (placement < -1 || placement > 1) return fail(MBIK_EINVAL, "placement must be -1 (automatic), 0 (LDS) or 1 (HBM)");
+	if (placement < -1 || placement > 2)
+		return fail(MBIK_EINVAL, "placement must be -1 (automatic), 0 (LDS), 1 (locals in device memory) or 2 (all state)");
 	p->locals_override = placement;
 	p->sched_K = -1;
 	return MBIK_OK;
@@ -1768,9 +1802,9 @@ int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const flo
 	// skeletons-per-block at each distinct residency (blocks per CU).  Every layout computes
 	// the same bits; only the time differs.
 	std::vector<std::tuple<int, int, int, int>> cands; // (spw override, interval, staging, locals in HBM)
-	for (int lh : {0, 1}) {
+	for (int lh : {0, 1, 2}) {
 		if (locals0 >= 0 && lh != locals0) continue;
-		p->host.locals_hbm = lh != 0;
+		p->host.state_hbm = lh;
 		for (int stg : {1, 0}) {
 			if (staging0 >= 0 && stg != staging0) continue;
 			p->host.staging = stg != 0;
@@ -1969,7 +2003,7 @@ int32_t mbik_group_solve(mbik_group *g, const int32_t *first, const int32_t *cou
 		if (!pose_in[i] || !pose_out[i] || (p->host.P > 0 && !targets[i])) return fail(MBIK_EINVAL, "null buffer");
 		int rc = p->host.P > 0 ? ensure_schedule(p, c) : MBIK_OK;
 		if (rc) return rc;
-		if (p->host.constraint_mode || p->host.P == 0 || p->host.locals_hbm) {
+		if (p->host.constraint_mode || p->host.P == 0 || p->host.state_hbm != 0) {
 			// constraint_mode plans have their own kernel, so do plans laid out with their
 			// locals in HBM; pinless plans only copy
 			rc = launch(p, f, c, pose_in[i], targets[i], pose_out[i], stream, p->host.iterations, 0, p->host.NS - 1);

@@ -134,7 +134,8 @@ class Plan:
         check(self._L.mbik_plan_set_heading_staging(self.h, int(staging)))
 
     def set_locals_placement(self, placement: int = -1):
-        """mbik_plan_set_locals_placement: 0 bone locals in LDS, 1 in device memory, -1 automatic."""
+        """mbik_plan_set_locals_placement: 0 state in LDS, 1 bone locals in device memory,
+        2 all per-skeleton state in device memory, -1 automatic."""
         check(self._L.mbik_plan_set_locals_placement(self.h, int(placement)))
 
     def autotune(self, pose_in_ptr: int, targets_ptr: int, pose_out_ptr: int, first: int = 0,

@@ -103,28 +103,31 @@ def test_staging_argument_check(mbik):
 @pytest.mark.parametrize("cfg,n", [(1, 8), (2, 48), (3, 48), (4, 16), (5, 6)])
 @pytest.mark.parametrize("staging", [1, 0])
 @pytest.mark.parametrize("stab", [0, 2])
-def test_locals_in_hbm_bitwise_vs_oracle(oracle, mbik, cfg, n, staging, stab):
-    """mbik_plan_set_locals_placement(1): the bone locals live in device memory during the
-    launch (sibling lanes exchange them through L2 across the row barriers); bitwise equal."""
+@pytest.mark.parametrize("placement", [1, 2])
+def test_state_in_hbm_bitwise_vs_oracle(oracle, mbik, cfg, n, staging, stab, placement):
+    """mbik_plan_set_locals_placement(1 | 2): the bone locals (1) or the whole per-skeleton
+    state (2, staged headings included) live in device memory during the launch; lanes
+    exchange them through L2 across the row and wave barriers; bitwise equal."""
     wl = W.generate(cfg, n, first=12000)
     ref = oracle.Oracle(wl, stabilization_passes=stab).solve(wl.pose, wl.targets, threads=8)
     plan = Plan.from_workload(wl, stabilization_passes=stab)
-    plan.set_locals_placement(1)
+    plan.set_locals_placement(placement)
     plan.set_heading_staging(staging)
     got = plan.solve_host(wl.pose, wl.targets)
-    assert_parity(got, ref, f"C{cfg} locals in HBM staging={staging} stab={stab}")
+    assert_parity(got, ref, f"C{cfg} state placement {placement} staging={staging} stab={stab}")
     plan.set_locals_placement(0)                          # back to LDS: same bits
     assert_parity(plan.solve_host(wl.pose, wl.targets), ref, f"C{cfg} locals back in LDS")
 
 
-def test_locals_in_hbm_subrange_and_group(oracle, mbik):
+@pytest.mark.parametrize("placement", [1, 2])
+def test_state_in_hbm_subrange_and_group(oracle, mbik, placement):
     """A subrange launch indexes the HBM locals by absolute skeleton; a group with such a plan
     launches it on its own and the results stay exact."""
     from many_bone_ik_amd.solver import Group
     wl = W.generate(2, 40, first=300)
     ref = oracle.Oracle(wl).solve(wl.pose, wl.targets, threads=8)
     plan = Plan.from_workload(wl)
-    plan.set_locals_placement(1)
+    plan.set_locals_placement(placement)
     import torch
     dev = torch.device("cuda", 0)
     pi = torch.from_numpy(wl.pose).to(dev)
