@@ -1801,37 +1801,45 @@ int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const flo
 	// Candidate layouts: for each heading-staging mode and checkpoint interval, the largest
 	// skeletons-per-block at each distinct residency (blocks per CU).  Every layout computes
 	// the same bits; only the time differs.
-	std::vector<std::tuple<int, int, int, int>> cands; // (spw override, interval, staging, locals in HBM)
-	for (int lh : {0, 1, 2}) {
-		if (locals0 >= 0 && lh != locals0) continue;
-		p->host.state_hbm = lh;
-		for (int stg : {1, 0}) {
-			if (staging0 >= 0 && stg != staging0) continue;
-			p->host.staging = stg != 0;
-			for (int c : {1, 2, 4, 1 << 20}) {
-				int last_blocks = -1;
-				for (int spw = 64; spw >= 1; spw--) {
-					mbik::build_schedule(p->host, lanes, count, spw, c, blocks_per_cu, p, p->cu_count);
-					if (p->host.spw != spw) continue; // capped by 64 / K or by LDS
-					const int blocks = blocks_per_cu(p, p->host.lds_block_bytes);
-					if (blocks != last_blocks) {
-						cands.push_back({spw, c, stg, lh});
-						last_blocks = blocks;
+	// Lane counts: the pinned one, or the widest sibling level and half of it (two sibling
+	// segments per lane: a longer chain, twice the skeletons per wave).
+	std::vector<int> lane_cands = {lanes};
+	if (lanes == 0 && p->host.K >= 2) lane_cands.push_back(p->host.K / 2);
+	std::vector<std::tuple<int, int, int, int, int>> cands; // (spw override, interval, staging, state placement, lanes)
+	for (int ln : lane_cands) {
+		for (int lh : {0, 1, 2}) {
+			if (locals0 >= 0 && lh != locals0) continue;
+			p->host.state_hbm = lh;
+			for (int stg : {1, 0}) {
+				if (staging0 >= 0 && stg != staging0) continue;
+				p->host.staging = stg != 0;
+				// with the whole state in device memory the interval does not change residency
+				const std::vector<int> intervals = lh == 2 ? std::vector<int>{1} : std::vector<int>{1, 2, 4, 1 << 20};
+				for (int c : intervals) {
+					int last_blocks = -1;
+					for (int spw = 64; spw >= 1; spw--) {
+						mbik::build_schedule(p->host, ln, count, spw, c, blocks_per_cu, p, p->cu_count);
+						if (p->host.spw != spw) continue; // capped by 64 / K or by LDS
+						const int blocks = blocks_per_cu(p, p->host.lds_block_bytes);
+						if (blocks != last_blocks) {
+							cands.push_back({spw, c, stg, lh, ln});
+							last_blocks = blocks;
+						}
 					}
 				}
+				if (p->host.hs_floats == 0) break; // nothing is staged: the no-staging layouts are the same
 			}
-			if (p->host.hs_floats == 0) break; // nothing is staged: the no-staging layouts are the same
 		}
 	}
 	hipEvent_t e0, e1;
 	if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return fail(MBIK_EHIP, "hipEventCreate");
 	float best_ms = 0.0f;
-	int best_spw = 0, best_c = 0, best_stg = 1, best_lh = 0, rc = MBIK_OK;
+	int best_spw = 0, best_c = 0, best_stg = 1, best_lh = 0, best_ln = lanes, rc = MBIK_OK;
 	std::vector<std::tuple<int, int, int, int, int>> seen; // resolved (K, spw, interval, staging, locals)
-	for (auto [spw, c, stg, lh] : cands) {
+	for (auto [spw, c, stg, lh, ln] : cands) {
 		p->spw_override = spw;
 		p->interval_override = c;
-		p->lanes_override = lanes;
+		p->lanes_override = ln;
 		p->staging_override = stg;
 		p->locals_override = lh;
 		if ((rc = ensure_schedule(p, count)) != MBIK_OK) break;
@@ -1856,6 +1864,7 @@ int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const flo
 			best_c = p->host.g_interval;
 			best_stg = stg;
 			best_lh = lh;
+			best_ln = ln;
 		}
 	}
 	(void)hipEventDestroy(e0);
@@ -1865,6 +1874,7 @@ int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const flo
 	p->interval_override = best_c;
 	p->staging_override = best_stg;
 	p->locals_override = best_lh;
+	p->lanes_override = best_ln;
 	return ensure_schedule(p, count);
 }
 
