@@ -14,7 +14,8 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/ktrace -o run --outpu
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o run --output-format csv -- python3 $B > $OUT/fetch.json 2> $OUT/fetch.log
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o run --output-format csv -- python3 $B > $OUT/write.json 2> $OUT/write.log
 N=$(python3 -c "import json,sys; print(json.loads(open('$OUT/ktrace.json').read().strip().splitlines()[-1])['config']['skeletons_per_gpu'])")
-python3 tools/traffic_from_pmc.py $(ls $OUT/fetch/run_counter_collection.csv) $(ls $OUT/write/run_counter_collection.csv) c${CFG}_$N profiles/traffic.json
+# the last 26 dispatches: 20 timed steps + 6 host-buffer frames, after autotune fixed the layout
+python3 tools/traffic_from_pmc.py $(ls $OUT/fetch/run_counter_collection.csv) $(ls $OUT/write/run_counter_collection.csv) c${CFG}_$N profiles/traffic.json --last 26
 cp profiles/traffic.json $OUT/traffic.json
 timeout -k 10 300 python3 bench.py --config $CFG > $OUT/bench.json 2> $OUT/bench.err
 cat $OUT/bench.json
