@@ -133,6 +133,11 @@ int32_t mbik_plan_set_heading_staging(mbik_plan *plan, int32_t staging);
  * only the block's topology copy).  Less LDS per skeleton, more skeletons resident per CU.
  * -1: automatic (mbik_plan_autotune times each).  Results do not depend on it. */
 int32_t mbik_plan_set_locals_placement(mbik_plan *plan, int32_t placement);
+/* Waves per SIMD the solve kernel is built for: 1 (default) the whole register file; 2 at
+ * most 256 registers (some spilled), so two blocks share a SIMD -- for launches too large to
+ * be resident at once.  -1: automatic (mbik_plan_autotune times both).  Plans with
+ * stabilization passes always use 1.  Results do not depend on it. */
+int32_t mbik_plan_set_waves_per_simd(mbik_plan *plan, int32_t waves);
 /* Re-derives the per-skeleton setup data (bone-direction frames, Kusudama cones, tangent
  * circles and twist frames -- what mbik_plan_create computes on the host from the setup
  * pose, ManyBoneIK3D::_bone_list_changed many_bone_ik_3d.cpp:1011-1068) on the GPU for

@@ -102,6 +102,8 @@ struct HostPlan {
 	// LDS; 2 all of it in device memory (LDS holds only the block's topology copy).  Less LDS
 	// per skeleton means more skeletons resident per CU, for L2 instead of LDS latency.
 	int32_t state_hbm = 0;
+	// Waves per SIMD the solve kernel's registers are sized for (1, or 2 with spills).
+	int32_t waves_per_simd = 1;
 	// Iteration-start globals kept in LDS only for checkpoint bones: every g_interval-th bone
 	// of a segment counted from its root (the root included) and every parent of a segment
 	// root; a bone-step rebuilds its parent's global from the nearest checkpoint above it.

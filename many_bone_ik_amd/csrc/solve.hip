@@ -1121,8 +1121,12 @@ __device__ __forceinline__ int xcd_block() {
 #endif
 }
 
-template <bool STAB, int PL>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MBIK_WAVES_PER_EU, MBIK_WAVES_PER_EU))) void mbik_solve_kernel(DevPlan t, int first, int count, const float *__restrict__ pose_in,
+// WPE: waves per SIMD the register budget is sized for.  1 (the default): the whole register
+// file, no spills.  2: at most 256 registers, some spilled to scratch, but two one-wave
+// blocks share a SIMD -- for launches whose skeletons no longer fit the chip at once and
+// whose state is not in LDS (mbik_plan_set_waves_per_simd; autotune decides).
+template <bool STAB, int PL, int WPE = MBIK_WAVES_PER_EU>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void mbik_solve_kernel(DevPlan t, int first, int count, const float *__restrict__ pose_in,
 		const float *__restrict__ targets, float *__restrict__ pose_out, int iterations, int seg_lo, int seg_hi) {
 	solve_block<STAB, PL>(t, xcd_block(), first, count, pose_in, targets, pose_out, iterations, seg_lo, seg_hi);
 }
@@ -1210,6 +1214,7 @@ struct mbik_plan {
 	int sched_K = -1, sched_c = -1, sched_staging = -1; // layout of the uploaded topology blob
 	int staging_override = -1;                           // mbik_plan_set_heading_staging; -1 = automatic
 	int locals_override = -1;                            // mbik_plan_set_locals_placement; -1 = automatic
+	int waves_override = -1;                             // mbik_plan_set_waves_per_simd; -1 = automatic
 	int sched_locals = -1;
 	float *d_locals = nullptr;                           // [N][B][12] for state_hbm 1
 	float *d_state = nullptr;                            // [N][state stride] for state_hbm 2
@@ -1293,12 +1298,16 @@ using SolveKernel = void (*)(DevPlan, int, int, const float *, const float *, fl
 SolveKernel solve_kernel_for(const mbik::HostPlan &h) {
 	static const SolveKernel ks[2][3] = {{mbik_solve_kernel<false, 0>, mbik_solve_kernel<false, 1>, mbik_solve_kernel<false, 2>},
 			{mbik_solve_kernel<true, 0>, mbik_solve_kernel<true, 1>, mbik_solve_kernel<true, 2>}};
+	static const SolveKernel k2[3] = {mbik_solve_kernel<false, 0, 2>, mbik_solve_kernel<false, 1, 2>, mbik_solve_kernel<false, 2, 2>};
 	static std::once_flag once;
 	std::call_once(once, [] {
 		for (auto &row : ks)
 			for (SolveKernel k : row) (void)hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+		for (SolveKernel k : k2) (void)hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 	});
-	return ks[h.stabilization_passes > 0 ? 1 : 0][std::min(2, std::max(0, (int)h.state_hbm))];
+	const int pl = std::min(2, std::max(0, (int)h.state_hbm));
+	if (h.waves_per_simd == 2 && h.stabilization_passes == 0) return k2[pl];
+	return ks[h.stabilization_passes > 0 ? 1 : 0][pl];
 }
 
 // Resident one-wave blocks per CU for a block's LDS size, from the runtime's occupancy
@@ -1323,6 +1332,7 @@ int ensure_schedule(mbik_plan *p, int64_t nlaunch) {
 	if (lanes == 0 && h.constraint_mode && p->cm_lanes > 0) lanes = p->cm_lanes;
 	h.staging = p->staging_override != 0;
 	h.state_hbm = h.constraint_mode ? 0 : std::max(0, p->locals_override);
+	h.waves_per_simd = (p->waves_override == 2 && !h.constraint_mode && h.stabilization_passes == 0) ? 2 : 1;
 	if (h.state_hbm == 1 && !p->d_locals) {
 		const size_t bytes = (size_t)h.N * h.B * 12 * sizeof(float);
 		if (hipMalloc(&p->d_locals, bytes) != hipSuccess) return fail(MBIK_ENOMEM, "hipMalloc locals");
@@ -1630,6 +1640,14 @@ int32_t mbik_plan_set_layout(mbik_plan *p, int32_t lanes, int32_t skeletons_per_
 	return MBIK_OK;
 }
 
+int32_t mbik_plan_set_waves_per_simd(mbik_plan *p, int32_t waves) {
+	if (!p) return fail(MBIK_EINVAL, "null plan");
+	if (waves != -1 && waves != 1 && waves != 2) return fail(MBIK_EINVAL, "waves_per_simd must be -1 (automatic), 1 or 2");
+	p->waves_override = waves;
+	p->sched_K = -1;
+	return MBIK_OK;
+}
+
 int32_t mbik_plan_set_locals_placement(mbik_plan *p, int32_t placement) {
 	if (!p) return fail(MBIK_EINVAL, "null plan");
 	if (placement < -1 || placement > 2)
@@ -1786,6 +1804,7 @@ int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const flo
 	const int lanes = p->lanes_override;
 	const int staging0 = p->staging_override;
 	const int locals0 = p->locals_override;
+	const int waves0 = p->waves_override;
 	{
 		// A launch whose skeletons are all resident at the default layout is bound by one
 		// skeleton's dependency chain; no layout shortens that, so there is nothing to time.
@@ -1793,6 +1812,7 @@ int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const flo
 		p->interval_override = 0;
 		p->staging_override = staging0 < 0 ? 1 : staging0;
 		p->locals_override = locals0 < 0 ? 0 : locals0;
+		p->waves_override = waves0 < 0 ? 1 : waves0;
 		int rc0 = ensure_schedule(p, count);
 		if (rc0 != MBIK_OK) return rc0;
 		if ((int64_t)blocks_per_cu(p, p->host.lds_block_bytes) * p->host.spw * p->cu_count >= count && p->host.g_interval == 1)
@@ -1805,10 +1825,16 @@ int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const flo
 	// segments per lane: a longer chain, twice the skeletons per wave).
 	std::vector<int> lane_cands = {lanes};
 	if (lanes == 0 && p->host.K >= 2) lane_cands.push_back(p->host.K / 2);
-	std::vector<std::tuple<int, int, int, int, int>> cands; // (spw override, interval, staging, state placement, lanes)
+	std::vector<std::tuple<int, int, int, int, int, int>> cands; // (spw override, interval, staging, state placement, lanes, waves)
+	for (int wv : {1, 2}) {
+	if (waves0 > 0 && wv != waves0) continue;
+	if (wv == 2 && p->host.stabilization_passes > 0) continue;
+	p->host.waves_per_simd = wv;
 	for (int ln : lane_cands) {
 		for (int lh : {0, 1, 2}) {
 			if (locals0 >= 0 && lh != locals0) continue;
+			// a second wave per SIMD only pays where LDS no longer bounds the blocks per CU
+			if (wv == 2 && lh == 0 && locals0 < 0) continue;
 			p->host.state_hbm = lh;
 			for (int stg : {1, 0}) {
 				if (staging0 >= 0 && stg != staging0) continue;
@@ -1822,7 +1848,7 @@ int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const flo
 						if (p->host.spw != spw) continue; // capped by 64 / K or by LDS
 						const int blocks = blocks_per_cu(p, p->host.lds_block_bytes);
 						if (blocks != last_blocks) {
-							cands.push_back({spw, c, stg, lh, ln});
+							cands.push_back({spw, c, stg, lh, ln, wv});
 							last_blocks = blocks;
 						}
 					}
@@ -1831,19 +1857,21 @@ int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const flo
 			}
 		}
 	}
+	}
 	hipEvent_t e0, e1;
 	if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return fail(MBIK_EHIP, "hipEventCreate");
 	float best_ms = 0.0f;
-	int best_spw = 0, best_c = 0, best_stg = 1, best_lh = 0, best_ln = lanes, rc = MBIK_OK;
-	std::vector<std::tuple<int, int, int, int, int>> seen; // resolved (K, spw, interval, staging, locals)
-	for (auto [spw, c, stg, lh, ln] : cands) {
+	int best_spw = 0, best_c = 0, best_stg = 1, best_lh = 0, best_ln = lanes, best_wv = 1, rc = MBIK_OK;
+	std::vector<std::tuple<int, int, int, int, int, int>> seen; // resolved (K, spw, interval, staging, locals, waves)
+	for (auto [spw, c, stg, lh, ln, wv] : cands) {
 		p->spw_override = spw;
 		p->interval_override = c;
 		p->lanes_override = ln;
 		p->staging_override = stg;
 		p->locals_override = lh;
+		p->waves_override = wv;
 		if ((rc = ensure_schedule(p, count)) != MBIK_OK) break;
-		const auto key = std::make_tuple(p->host.K, p->host.spw, p->host.g_interval, stg, lh);
+		const auto key = std::make_tuple(p->host.K, p->host.spw, p->host.g_interval, stg, lh, wv);
 		if (std::find(seen.begin(), seen.end(), key) != seen.end()) continue;
 		seen.push_back(key);
 		if ((rc = launch(p, first, count, pose_in, targets, pose_out, st, p->host.iterations, 0, p->host.NS - 1)) != MBIK_OK) break;
@@ -1865,6 +1893,7 @@ int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const flo
 			best_stg = stg;
 			best_lh = lh;
 			best_ln = ln;
+			best_wv = wv;
 		}
 	}
 	(void)hipEventDestroy(e0);
@@ -1875,6 +1904,7 @@ int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const flo
 	p->staging_override = best_stg;
 	p->locals_override = best_lh;
 	p->lanes_override = best_ln;
+	p->waves_override = best_wv;
 	return ensure_schedule(p, count);
 }
 

@@ -138,6 +138,10 @@ class Plan:
         2 all per-skeleton state in device memory, -1 automatic."""
         check(self._L.mbik_plan_set_locals_placement(self.h, int(placement)))
 
+    def set_waves_per_simd(self, waves: int = -1):
+        """mbik_plan_set_waves_per_simd: 1 or 2 waves per SIMD, -1 automatic."""
+        check(self._L.mbik_plan_set_waves_per_simd(self.h, int(waves)))
+
     def autotune(self, pose_in_ptr: int, targets_ptr: int, pose_out_ptr: int, first: int = 0,
                  count: int | None = None, stream: int = 0):
         """mbik_plan_autotune: time candidate layouts on this batch, keep the fastest."""

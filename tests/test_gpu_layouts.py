@@ -147,3 +147,22 @@ def test_state_in_hbm_subrange_and_group(oracle, mbik, placement):
     torch.cuda.synchronize()
     assert_parity(po1.cpu().numpy(), ref, "group: HBM-locals plan")
     assert_parity(po3.cpu().numpy(), ref3, "group: LDS plan")
+
+
+@pytest.mark.parametrize("cfg,n", [(2, 48), (3, 48), (4, 16), (5, 6)])
+@pytest.mark.parametrize("placement", [0, 1, 2])
+def test_two_waves_per_simd_bitwise_vs_oracle(oracle, mbik, cfg, n, placement):
+    """mbik_plan_set_waves_per_simd(2): the 256-register build (spilling to scratch) computes
+    the same bits."""
+    wl = W.generate(cfg, n, first=15000)
+    ref = oracle.Oracle(wl).solve(wl.pose, wl.targets, threads=8)
+    plan = Plan.from_workload(wl)
+    plan.set_waves_per_simd(2)
+    plan.set_locals_placement(placement)
+    assert_parity(plan.solve_host(wl.pose, wl.targets), ref, f"C{cfg} 2 waves/SIMD placement {placement}")
+
+
+def test_waves_argument_check(mbik):
+    plan = Plan.from_workload(W.generate(3, 2))
+    with pytest.raises(_lib.MbikError):
+        plan.set_waves_per_simd(3)
