@@ -236,6 +236,8 @@ def main():
                    "cones_per_bone": wl.topo.cones_per_bone, "iterations": wl.topo.iterations,
                    "lanes_per_skeleton": info["lanes_per_skeleton"], "skeletons_per_block": info["skeletons_per_block"],
                    "lds_bytes_per_block": info["lds_bytes_per_block"],
+                   "layout": {k: info[k] for k in ("checkpoint_interval", "heading_staging", "state_placement",
+                                                   "waves_per_simd")},
                    "parallelism": f"dp{world} (skeleton shards, no data-path collective)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

@@ -50,7 +50,7 @@ extern "C" {
 #define MBIK_EUNSUPPORTED (-4)
 #define MBIK_ENODEV (-5)
 
-#define MBIK_ABI_VERSION 1
+#define MBIK_ABI_VERSION 2
 
 typedef struct mbik_plan mbik_plan;
 typedef struct mbik_group mbik_group;
@@ -104,6 +104,10 @@ typedef struct mbik_plan_info {
 	double algorithmic_bytes_per_skeleton; /* pose in/out + targets + plan tables read once */
 	double algorithmic_flops_per_skeleton; /* SURVEY.md §8(d) per-bone-step formula x bone-steps x iterations */
 	int64_t lds_bytes_per_block;       /* LDS of one launch block (spw skeletons + topology tables) */
+	int32_t checkpoint_interval;       /* iteration-start globals kept every n-th bone (1 << 20: segment roots only) */
+	int32_t heading_staging;           /* mbik_plan_set_heading_staging in effect (0 / 1) */
+	int32_t state_placement;           /* mbik_plan_set_locals_placement in effect (0 / 1 / 2) */
+	int32_t waves_per_simd;            /* mbik_plan_set_waves_per_simd in effect (1 / 2) */
 } mbik_plan_info;
 
 /* Builds the per-topology tables and the per-skeleton setup data for skeletons

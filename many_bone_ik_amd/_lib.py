@@ -56,7 +56,9 @@ class MbikPlanInfo(C.Structure):
                 ("lanes_per_skeleton", C.c_int32), ("skeletons_per_block", C.c_int32),
                 ("max_headings", C.c_int32), ("device", C.c_int32), ("device_bytes", C.c_int64),
                 ("algorithmic_bytes_per_skeleton", C.c_double),
-                ("algorithmic_flops_per_skeleton", C.c_double), ("lds_bytes_per_block", C.c_int64)]
+                ("algorithmic_flops_per_skeleton", C.c_double), ("lds_bytes_per_block", C.c_int64),
+                ("checkpoint_interval", C.c_int32), ("heading_staging", C.c_int32), ("state_placement", C.c_int32),
+                ("waves_per_simd", C.c_int32)]
 
 
 class MbikError(RuntimeError):

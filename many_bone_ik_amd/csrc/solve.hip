@@ -1617,6 +1617,10 @@ int32_t mbik_plan_get_info(const mbik_plan *p, mbik_plan_info *o) {
 	o->algorithmic_bytes_per_skeleton = p->alg_bytes;
 	o->algorithmic_flops_per_skeleton = p->alg_flops;
 	o->lds_bytes_per_block = h.constraint_mode ? (int64_t)cmode_lds_bytes(p) : p->host.lds_block_bytes;
+	o->checkpoint_interval = h.g_interval;
+	o->heading_staging = h.staging ? 1 : 0;
+	o->state_placement = h.state_hbm;
+	o->waves_per_simd = h.waves_per_simd;
 	return MBIK_OK;
 }
 
