@@ -993,7 +993,7 @@ __device__ __forceinline__ void write_nonfinite(const DevPlan &t, bool valid, bo
 #define MBIK_WAVES_PER_EU 1
 #endif
 // The solve of one block (blk = the plan-local block index after the XCD remap).
-template <bool STAB, int PL>
+template <bool STAB, int PL, bool HOIST = true>
 __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int count, const float *__restrict__ pose_in,
 		const float *__restrict__ targets, float *__restrict__ pose_out, int iterations, int seg_lo, int seg_hi) {
 	extern __shared__ float4 lds4[];
@@ -1077,7 +1077,9 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 				// the same effector data at every bone-step: load it once for the segment.
 				const int seg = task.x, e0 = t.seg_eff_off[seg];
 				EffPre pre;
-				const bool hoist = !STAB && t.seg_eff_off[seg + 1] - e0 == 1 && (task.z == 1 || t.seg_nh[seg] == 1);
+				// (not in the two-waves-per-SIMD build: the hoisted data's ~66 registers are what
+				// pushes that build past 256 and into scratch spills)
+				const bool hoist = HOIST && !STAB && t.seg_eff_off[seg + 1] - e0 == 1 && (task.z == 1 || t.seg_nh[seg] == 1);
 				if (hoist) load_eff(t, t.seg_effs[e0], TG, s, t.seg_hw + t.seg_hw_off[seg] + t.seg_eff_hoff[e0], pre);
 				for (int k = t.seg_bone_off[seg]; k < t.seg_bone_off[seg + 1]; k++)
 					bone_step<STAB>(t, seg, k, task.y, task.z, s, L, G, TG, ST, SF, HS, OE, MS, prev_dev, pre, hoist MBIK_PROF_ARG);
@@ -1128,7 +1130,7 @@ __device__ __forceinline__ int xcd_block() {
 template <bool STAB, int PL, int WPE = MBIK_WAVES_PER_EU>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void mbik_solve_kernel(DevPlan t, int first, int count, const float *__restrict__ pose_in,
 		const float *__restrict__ targets, float *__restrict__ pose_out, int iterations, int seg_lo, int seg_hi) {
-	solve_block<STAB, PL>(t, xcd_block(), first, count, pose_in, targets, pose_out, iterations, seg_lo, seg_hi);
+	solve_block<STAB, PL, WPE == 1>(t, xcd_block(), first, count, pose_in, targets, pose_out, iterations, seg_lo, seg_hi);
 }
 
 // A heterogeneous batch (mbik_group_solve): several plans -- distinct rigs -- in one launch.
