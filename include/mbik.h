@@ -158,10 +158,14 @@ int32_t mbik_plan_setup_tables(const mbik_plan *plan, float *D, float *CF, doubl
 /* Diagnostic: how many one-wave blocks using lds_bytes_per_block of LDS one CU of the plan's
  * device holds at once (the runtime occupancy query for the plan's kernel). */
 int32_t mbik_plan_resident_blocks(const mbik_plan *plan, int64_t lds_bytes_per_block);
-/* Times candidate layouts (checkpoint interval x skeletons per block) on a real batch and
- * keeps the fastest as the plan's layout.  Runs the solve several times into pose_out
- * (identical results); synchronizes hip_stream.  The chosen layout is fixed afterwards;
- * mbik_plan_set_layout(plan, 0, 0, 0) returns to the automatic one. */
+/* Times candidate layouts on a real batch and keeps the fastest as the plan's layout: lanes
+ * per skeleton (the widest sibling level or half of it), skeletons per block, checkpoint
+ * interval, heading staging, state placement and waves per SIMD; dimensions pinned by the
+ * setters above (a value other than 0 / -1) are kept.  A launch that is fully resident at the
+ * default layout is left as it is (one skeleton's chain bounds it).  Runs the solve several
+ * times into pose_out (identical results); synchronizes hip_stream.  The chosen layout is
+ * fixed afterwards; mbik_plan_set_layout(plan, 0, 0, 0) and the staging / placement / waves
+ * setters with -1 return to the defaults. */
 int32_t mbik_plan_autotune(mbik_plan *plan, int32_t first, int32_t count, const float *pose_in, const float *targets,
 		float *pose_out, void *hip_stream);
 
