@@ -166,3 +166,34 @@ def test_waves_argument_check(mbik):
     plan = Plan.from_workload(W.generate(3, 2))
     with pytest.raises(_lib.MbikError):
         plan.set_waves_per_simd(3)
+
+
+@pytest.mark.parametrize("cfg,n,pin", [(3, 65536, None), (5, 16384, (8, 8, 1, 0, 2, 2))])
+def test_tuned_full_size_layouts_are_exact(oracle, mbik, cfg, n, pin):
+    """Full-size launches on the layouts autotune picks for them (C3: autotuned here; C5: the
+    layout its autotune picks, pinned -- 8 lanes x 8, unstaged, all state in device memory, two
+    waves per SIMD); oracle spot checks at the start, middle and end of the batch."""
+    import torch
+    wl = W.generate(cfg, n)
+    plan = Plan.from_workload(wl)
+    dev = torch.device("cuda", 0)
+    pi = torch.from_numpy(wl.pose).to(dev)
+    tg = torch.from_numpy(wl.targets).to(dev)
+    po = torch.empty_like(pi)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    if pin is None:
+        plan.autotune(pi.data_ptr(), tg.data_ptr(), po.data_ptr(), 0, n, st)
+    else:
+        lanes, spw, interval, staging, placement, waves = pin
+        plan.set_layout(lanes, spw, interval)
+        plan.set_heading_staging(staging)
+        plan.set_locals_placement(placement)
+        plan.set_waves_per_simd(waves)
+    plan.solve(pi.data_ptr(), tg.data_ptr(), po.data_ptr(), 0, n, st)
+    torch.cuda.synchronize()
+    got = po.cpu().numpy()
+    info = plan.info()
+    for first in (0, n // 2 - 3, n - 6):
+        sub = W.generate(cfg, 6, first=first)
+        ref = oracle.Oracle(sub).solve(sub.pose, sub.targets, threads=8)
+        assert_parity(got[first:first + 6], ref, f"C{cfg} tuned layout {info} @{first}")
