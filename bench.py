@@ -137,7 +137,7 @@ def main():
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     wall_max = float(elapsed.item())
 
-    gather_ms = None
+    gather_ms = gather_root_ms = None
     if dist:
         parts = [torch.empty_like(pose_out) for _ in range(world)]
         dist.barrier()
@@ -148,6 +148,20 @@ def main():
         gt = torch.tensor([time.perf_counter() - g0], dtype=torch.float64, device=dev)
         dist.all_reduce(gt, op=dist.ReduceOp.MAX)
         gather_ms = float(gt.item()) * 1e3
+        # SURVEY §8(e)'s variant: every rank sends its shard to rank 0 only (one xGMI link
+        # each).  Reported beside the solve, never part of `value`; a failure is reported too.
+        try:
+            from many_bone_ik_amd.dist import gather_poses_to_root
+            dist.barrier()
+            torch.cuda.synchronize(dev)
+            g0 = time.perf_counter()
+            gather_poses_to_root(pose_out, n * world, root=0)
+            torch.cuda.synchronize(dev)
+            gt = torch.tensor([time.perf_counter() - g0], dtype=torch.float64, device=dev)
+            dist.all_reduce(gt, op=dist.ReduceOp.MAX)
+            gather_root_ms = float(gt.item()) * 1e3
+        except Exception as e:  # noqa: BLE001 -- measurement only
+            gather_root_ms = f"error: {e}"
 
     # PCIe-inclusive rate (host buffers in, solve, host buffers out): reported, never `value`
     pcie = None
@@ -249,6 +263,7 @@ def main():
                  "note": "SURVEY.md §8(d) flop formula; the bound that applies to this path (DESIGN.md §5)"},
         "issue": issue,
         "gather_ms": gather_ms,
+        "gather_to_root_ms": gather_root_ms,
         "pcie_inclusive": pcie,
         "parity": parity,
     }

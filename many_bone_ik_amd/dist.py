@@ -37,3 +37,25 @@ def gather_poses(pose_out, total: int, group=None):
     dist.all_gather(parts, pad, group=group)
     assert counts[rank] == pose_out.shape[0]
     return torch.cat([p[:c] for p, c in zip(parts, counts)], dim=0)
+
+
+def gather_poses_to_root(pose_out, total: int, root: int = 0, group=None):
+    """Gather every rank's pose shard onto `root` only (the ranks send, the
+    root receives world-1 shards, one per xGMI link in parallel -- RCCL send/recv under the
+    "nccl" backend).  Returns the [total, B, 10] tensor on `root`, None elsewhere."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    counts = [shard_range(r, world, total)[1] for r in range(world)]
+    cmax = max(counts)
+    assert counts[rank] == pose_out.shape[0]
+    pad = pose_out
+    if pose_out.shape[0] < cmax:
+        pad = torch.zeros((cmax,) + tuple(pose_out.shape[1:]), dtype=pose_out.dtype, device=pose_out.device)
+        pad[: pose_out.shape[0]] = pose_out
+    parts = [torch.empty_like(pad) for _ in range(world)] if rank == root else None
+    dist.gather(pad, gather_list=parts, dst=root, group=group)
+    if rank != root:
+        return None
+    return torch.cat([p[:c] for p, c in zip(parts, counts)], dim=0)

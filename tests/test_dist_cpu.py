@@ -25,12 +25,16 @@ def _worker(rank, world, port, total, out_path):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from many_bone_ik_amd import workloads as W
-    from many_bone_ik_amd.dist import gather_poses
+    from many_bone_ik_amd.dist import gather_poses, gather_poses_to_root
     from oracle import pyoracle as po
     first, count = shard_range(rank, world, total)
     wl = W.generate(2, count, first=first)
     out = po.Oracle(wl).solve(wl.pose, wl.targets)      # CPU stand-in for the per-rank solve
     full = gather_poses(torch.from_numpy(out), total)
+    rooted = gather_poses_to_root(torch.from_numpy(out), total, root=world - 1)
+    assert (rooted is None) == (rank != world - 1)
+    if rank == world - 1:
+        assert np.array_equal(rooted.numpy().view(np.uint32), full.numpy().view(np.uint32))
     if rank == 0:
         np.save(out_path, full.numpy())
     dist.destroy_process_group()
