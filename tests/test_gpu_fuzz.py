@@ -60,3 +60,23 @@ def test_random_configuration_bitwise(oracle, mbik, seed):
     plan = Plan.from_workload(wl, lanes=lanes, stabilization_passes=stab)
     got = plan.solve_host(wl.pose, wl.targets)
     assert_parity(got, ref, f"fuzz seed {seed} (B={wl.bone_count}, stab={stab}, lanes={lanes})")
+
+
+@pytest.mark.parametrize("seed", range(N_CASES))
+def test_random_configuration_random_layout_bitwise(oracle, mbik, seed):
+    """The same random rigs on a random launch layout: heading staging, state placement
+    (LDS / locals / all in device memory), waves per SIMD, checkpoint interval and skeletons
+    per block -- still bitwise equal to the oracle."""
+    wl, stab, lanes = random_case(seed)
+    rng = np.random.default_rng(5000 + seed)
+    ref = oracle.Oracle(wl, stabilization_passes=stab).solve(wl.pose, wl.targets, threads=4)
+    plan = Plan.from_workload(wl, stabilization_passes=stab)
+    staging, placement, waves = int(rng.integers(0, 2)), int(rng.integers(0, 3)), int(rng.integers(1, 3))
+    interval, spw = int(rng.choice([0, 1, 2, 3, 1 << 20])), int(rng.choice([0, 1, 3, 5]))
+    plan.set_layout(lanes, spw, interval)
+    plan.set_heading_staging(staging)
+    plan.set_locals_placement(placement)
+    plan.set_waves_per_simd(waves)
+    got = plan.solve_host(wl.pose, wl.targets)
+    assert_parity(got, ref, f"fuzz seed {seed} layout staging={staging} placement={placement} waves={waves} "
+                            f"interval={interval} spw={spw} lanes={lanes} stab={stab}")
