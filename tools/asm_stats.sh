@@ -3,7 +3,7 @@
 set -e
 cd "$(dirname "$0")/.."
 mkdir -p build/asm
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -Wno-unused-result --cuda-device-only -S \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-slp-vectorize -Wno-unused-result --cuda-device-only -S \
   "$@" many_bone_ik_amd/csrc/solve.hip -o build/asm/solve.s 2>/dev/null
 python3 - <<'PY'
 import re
