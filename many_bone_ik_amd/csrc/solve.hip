@@ -24,6 +24,7 @@
 
 #include <algorithm>
 #include <tuple>
+#include <type_traits>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -85,7 +86,7 @@ struct DevPlan {
 	// mbik_solve_checked: per-skeleton flag, 1 when any bone's solved basis was non-finite and
 	// was written as the identity rotation (ik_bone_3d.cpp:174-176); null otherwise.
 	unsigned char *nonfinite = nullptr;
-	// state_hbm 1: the bone locals of skeleton s at Lg + s * 12 * B; state_hbm 2: its whole
+	// state_hbm 1: the bone locals, [N/kLocTile][B][3][kLocTile][4] (LocTiled); state_hbm 2: the whole
 	// state at Sg + s * state_stride (the LDS layout of one skeleton)
 	float *Lg = nullptr, *Sg = nullptr;
 	int state_stride = 0;
@@ -110,6 +111,36 @@ __device__ __forceinline__ void st_x(float *p, const X3 &t) {
 	*reinterpret_cast<float4 *>(p + 4) = make_float4(t.b.r[1].y, t.b.r[1].z, t.b.r[2].x, t.b.r[2].y);
 	*reinterpret_cast<float4 *>(p + 8) = make_float4(t.b.r[2].z, t.o.x, t.o.y, t.o.z);
 }
+// A skeleton's bone locals: transform i's three float4 quads at p + BS*i + QS*{0,1,2}.
+// LocContig (BS 12, QS 4) is one skeleton's [B][12] block (LDS, or the whole state in device
+// memory); LocTiled interleaves the quads of kLocTile consecutive skeletons,
+// [N/kLocTile][B][3][kLocTile][4], so the lanes of one role in a wave (consecutive skeletons,
+// same bone) read whole cache lines.
+constexpr int kLocTile = 16;
+template <int BS, int QS>
+struct LocV {
+	float *p;
+	__device__ __forceinline__ X3 ld(int i) const {
+		const float *q = p + BS * i;
+		const float4 a = *reinterpret_cast<const float4 *>(q);
+		const float4 b = *reinterpret_cast<const float4 *>(q + QS);
+		const float4 c = *reinterpret_cast<const float4 *>(q + 2 * QS);
+		X3 t;
+		t.b.r[0] = v3(a.x, a.y, a.z);
+		t.b.r[1] = v3(a.w, b.x, b.y);
+		t.b.r[2] = v3(b.z, b.w, c.x);
+		t.o = v3(c.y, c.z, c.w);
+		return t;
+	}
+	__device__ __forceinline__ void st(int i, const X3 &t) const {
+		float *q = p + BS * i;
+		*reinterpret_cast<float4 *>(q) = make_float4(t.b.r[0].x, t.b.r[0].y, t.b.r[0].z, t.b.r[1].x);
+		*reinterpret_cast<float4 *>(q + QS) = make_float4(t.b.r[1].y, t.b.r[1].z, t.b.r[2].x, t.b.r[2].y);
+		*reinterpret_cast<float4 *>(q + 2 * QS) = make_float4(t.b.r[2].z, t.o.x, t.o.y, t.o.z);
+	}
+};
+using LocContig = LocV<12, 4>;
+using LocTiled = LocV<12 * kLocTile, 4 * kLocTile>;
 // SoA per-skeleton tables: element (item, field) of skeleton s.
 #ifdef MBIK_ABLATE_SOA
 #define MBIK_SOA_S(s) ((s) & 15) // timing experiment only: a hot 16-skeleton working set
@@ -293,7 +324,8 @@ __device__ __forceinline__ void heading_terms(const EffPre &p, const X3 &E, V3 o
 // oe_mode (stabilization, ik_bone_segment_3d.cpp:135-176): 0 plain; 1 also record the target
 // headings' origin in OE; 2 take that origin from OE (target headings are built once per
 // bone-step, before the retry loop, while tip headings are rebuilt on every pass).
-__device__ __forceinline__ void effector_headings(const DevPlan &t, const EffPre &p, int b, const X3 &Gb, const float *L,
+template <class LV>
+__device__ __forceinline__ void effector_headings(const DevPlan &t, const EffPre &p, int b, const X3 &Gb, const LV &L,
 		const float *ST, const int *SF, Headings &H, float *OE = nullptr, int oe_mode = 0) {
 	const int e = p.e;
 	X3 E;
@@ -306,10 +338,10 @@ __device__ __forceinline__ void effector_headings(const DevPlan &t, const EffPre
 		int d = t.bone_depth[b] + 1;
 		if (d <= de) {
 			// software-pipelined: the next path bone's local pose loads during this product
-			X3 Ln = ld_x(L + 12 * t.eff_path[off + d]);
+			X3 Ln = L.ld(t.eff_path[off + d]);
 			for (; d < de; d++) {
 				const X3 Lc = Ln;
-				Ln = ld_x(L + 12 * t.eff_path[off + d + 1]);
+				Ln = L.ld(t.eff_path[off + d + 1]);
 				X = X * Lc;
 			}
 			X = X * Ln;
@@ -325,7 +357,8 @@ __device__ __forceinline__ void effector_headings(const DevPlan &t, const EffPre
 	}
 	heading_terms(p, E, oe, Gb.o, H);
 }
-__device__ __forceinline__ void effector_headings(const DevPlan &t, int e, int b, const X3 &Gb, const float *L,
+template <class LV>
+__device__ __forceinline__ void effector_headings(const DevPlan &t, int e, int b, const X3 &Gb, const LV &L,
 		const float *TG, const float *ST, const int *SF, size_t s, const double *hw, Headings &H, float *OE = nullptr,
 		int oe_mode = 0, const B3 *Db = nullptr) {
 	EffPre p;
@@ -506,8 +539,8 @@ __device__ __forceinline__ void qcp_terms(const V3 wc1, const V3 c1, const V3 c2
 }
 // STAB: the plan has stabilization passes (a separate instantiation keeps the retry loop and
 // its LDS staging out of the default kernel).
-template <bool STAB>
-__device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j, int m, size_t s, float *L, const float *G, const float *TG,
+template <bool STAB, class LV>
+__device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j, int m, size_t s, const LV &L, const float *G, const float *TG,
 		float *ST, int *SF, float *HS, float *OE, float *MS, double &prev_dev, const EffPre &pre, bool hoist, bool dbh MBIK_PROF_PARAM) {
 	MBIK_PROF_T(pt0);
 #ifdef MBIK_PROF
@@ -526,15 +559,15 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 			P = ld_x(G + 12 * t.bone_gslot[pp]);
 		} else {
 			P = ld_x(G + 12 * t.bone_gslot[t.seg_bones[kc]]);
-			for (int q = kc - 1; q > k; q--) P = P * ld_x(L + 12 * t.seg_bones[q]);
+			for (int q = kc - 1; q > k; q--) P = P * L.ld(t.seg_bones[q]);
 		}
 	}
 	const B3 Pinv = inverse(P.b);
 	const bool stab = STAB && (t.seg_flags[seg] & mbik::SF_STAB) != 0;
-	const X3 Lprev = ld_x(L + 12 * b); // prev_transform (:136)
+	const X3 Lprev = L.ld(b); // prev_transform (:136)
 	for (int attempt = 0;; attempt++) {
 	const int oe_mode = stab ? (attempt == 0 ? 1 : 2) : 0;
-	X3 Lb = ld_x(L + 12 * b);
+	X3 Lb = L.ld(b);
 	const X3 Gb = hasP ? P * Lb : Lb;
 	const SlerpTo sto = slerp_to(Gb.b);
 	const bool translate = (t.seg_flags[seg] & mbik::SF_TRANSLATE) != 0;
@@ -888,7 +921,7 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 		Lb.b = rotation;
 	}
 	{
-		st_x(L + 12 * b, Lb);
+		L.st(b, Lb);
 		// A swing with no propagating twist leaves b's bone-direction cache stale until the
 		// parent's set_global_pose (IKNode3D::rotate_local_with_global, ik_node_3d.cpp:56-67).
 		if ((flags & mbik::BF_PINNED) && swung && !twist_changed) {
@@ -937,7 +970,7 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 		// reject: set_pose(prev_transform) -> IKNode3D::set_transform propagates only when the
 		// local transform changes (ik_node_3d.cpp:69-75), refreshing b's subtree caches.
 		if (!eq(Lb, Lprev)) {
-			st_x(L + 12 * b, Lprev);
+			L.st(b, Lprev);
 			if (flags & mbik::BF_PINNED) SF[t.bone_pin[b]] = 0;
 			for (int c = t.bone_child_eff_off[b]; c < t.bone_child_eff_off[b + 1]; c++) SF[t.bone_child_effs[c]] = 0;
 		}
@@ -953,12 +986,13 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 }
 
 // Iteration-start globals of one segment, root -> tip (IKNode3D::get_global_transform).
-__device__ void global_pass(const DevPlan &t, int seg, const float *L, float *G) {
+template <class LV>
+__device__ void global_pass(const DevPlan &t, int seg, const LV &L, float *G) {
 	X3 Gprev = xid();
 	for (int k = t.seg_bone_off[seg + 1] - 1; k >= t.seg_bone_off[seg]; k--) {
 		const int b = t.seg_bones[k];
 		const int pp = t.bone_pose_parent[b];
-		X3 Lb = ld_x(L + 12 * b);
+		X3 Lb = L.ld(b);
 		X3 Gb;
 		if (k < t.seg_bone_off[seg + 1] - 1) Gb = Gprev * Lb; // parent = the bone just done
 		else Gb = pp >= 0 ? ld_x(G + 12 * t.bone_gslot[pp]) * Lb : (pp == mbik::POSE_PARENT_ORIGIN ? xid() * Lb : Lb);
@@ -1032,16 +1066,18 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 	const int B = t.B, P = t.P, K = t.K;
 	// PL (HostPlan::state_hbm): 0 the state in LDS; 1 the locals in device memory (L2-resident
 	// during the launch), the rest in LDS; 2 all of it in device memory
-	float *L, *G;
+	using LV = std::conditional_t<PL == 1, LocTiled, LocContig>;
+	LV L;
+	float *G;
 	if constexpr (PL == 2) {
-		L = t.Sg + s * (size_t)t.state_stride;
-		G = L + 12 * B;
+		L.p = t.Sg + s * (size_t)t.state_stride;
+		G = L.p + 12 * B;
 	} else if constexpr (PL == 1) {
-		L = t.Lg + s * 12 * (size_t)B;
+		L.p = t.Lg + (s / kLocTile) * (size_t)(12 * kLocTile) * B + (s % kLocTile) * 4;
 		G = lds + (size_t)g * t.lds_stride;
 	} else {
-		L = lds + (size_t)g * t.lds_stride;
-		G = L + 12 * B;
+		L.p = lds + (size_t)g * t.lds_stride;
+		G = L.p + 12 * B;
 	}
 	float *TG = G + 12 * t.n_gck;
 	float *ST = TG + 12 * P;
@@ -1051,7 +1087,7 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 	float *MS = OE + 3 * P;                        // stabilization only: 7 per pin
 	if (valid) {
 		for (int b = role; b < B; b += K)
-			if (t.bone_flags[b] & mbik::BF_IN_LIST) st_x(L + 12 * b, pose_to_xform(pose_in + ((size_t)local * B + b) * 10));
+			if (t.bone_flags[b] & mbik::BF_IN_LIST) L.st(b, pose_to_xform(pose_in + ((size_t)local * B + b) * 10));
 		for (int e = role; e < P; e += K) {
 			const float *src = targets + ((size_t)local * P + e) * 12;
 			for (int f = 0; f < 12; f++) TG[12 * e + f] = src[f];
@@ -1098,7 +1134,7 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 		for (int b = role; b < B; b += K) {
 			float *dst = pose_out + ((size_t)local * B + b) * 10;
 			if (t.bone_flags[b] & mbik::BF_IN_LIST) {
-				bad |= write_pose(ld_x(L + 12 * b), dst);
+				bad |= write_pose(L.ld(b), dst);
 			} else {
 				const float *src = pose_in + ((size_t)local * B + b) * 10;
 				for (int f = 0; f < 10; f++) dst[f] = src[f];
@@ -1341,7 +1377,8 @@ int ensure_schedule(mbik_plan *p, int64_t nlaunch) {
 	h.state_hbm = h.constraint_mode ? 0 : std::max(0, p->locals_override);
 	h.waves_per_simd = (p->waves_override == 2 && !h.constraint_mode && h.stabilization_passes == 0) ? 2 : 1;
 	if (h.state_hbm == 1 && !p->d_locals) {
-		const size_t bytes = (size_t)h.N * h.B * 12 * sizeof(float);
+		// LocTiled: whole tiles of kLocTile skeletons
+		const size_t bytes = (size_t)((h.N + kLocTile - 1) / kLocTile) * kLocTile * h.B * 12 * sizeof(float);
 		if (hipMalloc(&p->d_locals, bytes) != hipSuccess) return fail(MBIK_ENOMEM, "hipMalloc locals");
 		p->allocs.push_back(p->d_locals);
 		p->device_bytes += (int64_t)bytes;
