@@ -1066,14 +1066,13 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 	const int B = t.B, P = t.P, K = t.K;
 	// PL (HostPlan::state_hbm): 0 the state in LDS; 1 the locals in device memory (L2-resident
 	// during the launch), the rest in LDS; 2 all of it in device memory
-	using LV = std::conditional_t<PL == 1, LocTiled, LocContig>;
+	using LV = std::conditional_t<PL >= 1, LocTiled, LocContig>;
 	LV L;
 	float *G;
+	if constexpr (PL >= 1) L.p = t.Lg + (s / kLocTile) * (size_t)(12 * kLocTile) * B + (s % kLocTile) * 4;
 	if constexpr (PL == 2) {
-		L.p = t.Sg + s * (size_t)t.state_stride;
-		G = L.p + 12 * B;
+		G = t.Sg + s * (size_t)t.state_stride + 12 * B;
 	} else if constexpr (PL == 1) {
-		L.p = t.Lg + (s / kLocTile) * (size_t)(12 * kLocTile) * B + (s % kLocTile) * 4;
 		G = lds + (size_t)g * t.lds_stride;
 	} else {
 		L.p = lds + (size_t)g * t.lds_stride;
@@ -1376,7 +1375,7 @@ int ensure_schedule(mbik_plan *p, int64_t nlaunch) {
 	h.staging = p->staging_override != 0;
 	h.state_hbm = h.constraint_mode ? 0 : std::max(0, p->locals_override);
 	h.waves_per_simd = (p->waves_override == 2 && !h.constraint_mode && h.stabilization_passes == 0) ? 2 : 1;
-	if (h.state_hbm == 1 && !p->d_locals) {
+	if (h.state_hbm >= 1 && !p->d_locals) {
 		// LocTiled: whole tiles of kLocTile skeletons
 		const size_t bytes = (size_t)((h.N + kLocTile - 1) / kLocTile) * kLocTile * h.B * 12 * sizeof(float);
 		if (hipMalloc(&p->d_locals, bytes) != hipSuccess) return fail(MBIK_ENOMEM, "hipMalloc locals");
