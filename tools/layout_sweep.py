@@ -1,4 +1,5 @@
-"""Time mbik_solve under explicit layouts: args cfg:n:lanes:spw:interval (0 = auto)."""
+"""Time mbik_solve under explicit layouts: args cfg:n:lanes:spw:interval[:placement:staging:waves] (0 = auto;
+placement / staging / waves default to the plan's own)."""
 import sys, json
 import torch
 sys.path.insert(0, '.')
@@ -8,13 +9,20 @@ from many_bone_ik_amd.solver import Plan
 dev = torch.device('cuda', 0)
 cache = {}
 for arg in sys.argv[1:]:
-    cfg, n, lanes, spw, interval = (int(x) for x in arg.split(':'))
+    f = [int(x) for x in arg.split(':')]
+    cfg, n, lanes, spw, interval = f[:5]
     if (cfg, n) not in cache:
         cache.clear()
         cache[(cfg, n)] = W.generate(cfg, n)
     wl = cache[(cfg, n)]
     p = Plan.from_workload(wl)
     p.set_layout(lanes, spw, interval)
+    if len(f) > 5:
+        p.set_locals_placement(f[5])
+    if len(f) > 6:
+        p.set_heading_staging(f[6])
+    if len(f) > 7:
+        p.set_waves_per_simd(f[7])
     pi = torch.from_numpy(wl.pose).to(dev); tg = torch.from_numpy(wl.targets).to(dev); po = torch.empty_like(pi)
     st = torch.cuda.current_stream(dev).cuda_stream
     p.solve(pi.data_ptr(), tg.data_ptr(), po.data_ptr(), 0, n, st); torch.cuda.synchronize()
