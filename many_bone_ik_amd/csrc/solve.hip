@@ -87,7 +87,7 @@ struct DevPlan {
 	// was written as the identity rotation (ik_bone_3d.cpp:174-176); null otherwise.
 	unsigned char *nonfinite = nullptr;
 	// state_hbm 1: the bone locals, [N/kLocTile][B][3][kLocTile][4] (LocTiled); state_hbm 2: the whole
-	// state at Sg + s * state_stride (the LDS layout of one skeleton)
+	// other state at Sg + s * state_stride (one skeleton's LDS layout after its locals)
 	float *Lg = nullptr, *Sg = nullptr;
 	int state_stride = 0;
 };
@@ -1071,7 +1071,7 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 	float *G;
 	if constexpr (PL >= 1) L.p = t.Lg + (s / kLocTile) * (size_t)(12 * kLocTile) * B + (s % kLocTile) * 4;
 	if constexpr (PL == 2) {
-		G = t.Sg + s * (size_t)t.state_stride + 12 * B;
+		G = t.Sg + s * (size_t)t.state_stride;
 	} else if constexpr (PL == 1) {
 		G = lds + (size_t)g * t.lds_stride;
 	} else {
@@ -1388,7 +1388,8 @@ int ensure_schedule(mbik_plan *p, int64_t nlaunch) {
 		mbik::build_schedule(h, kCmodeLanes, nlaunch, p->spw_override, p->interval_override, blocks_per_cu, p, p->cu_count);
 	if (h.state_hbm == 2) {
 		// the whole state in device memory: one skeleton's LDS layout per skeleton
-		const int stride = (mbik::state_floats_per_skeleton(h) + 3) & ~3;
+		// (the locals live in the tiled area, d_locals)
+		const int stride = (mbik::state_floats_per_skeleton(h) - 12 * h.B + 3) & ~3;
 		const size_t need = (size_t)h.N * stride;
 		if (need > p->d_state_floats) {
 			void *a = nullptr;
