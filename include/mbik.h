@@ -233,6 +233,28 @@ int32_t mbik_describe_topology(const mbik_skeleton_desc *desc, const mbik_config
  * exactly one of them is NaN.  Both must be 0 (gd_math.h: gd_sqrt). */
 int32_t mbik_selftest_math(int32_t device, uint64_t out[2]);
 
+/* Device self-test of the solve's transcendental call sites against values the caller
+ * computed with the host's libm (the reference's: Godot's Math::sin/cos/acos call ::sinf,
+ * ::cosf, ::acosf and ::sin/::cos; glibc on Linux x86-64).  For fn = SINF, COSF, ACOSF,
+ * SLERP_SCALE0 and COS_F64_OF_F32 the inputs are the float bit patterns first ..
+ * first+count-1 (first + count <= 2^32); for COS_F64 they are `inputs` (device, count
+ * doubles).  expected (device): count floats (SINF..SLERP_SCALE0) or doubles (the two COS
+ * variants).  out[0] = results whose bits differ (two NaNs compare equal), out[1] = the
+ * lowest differing index (~0 when none).  Synchronizes hip_stream.
+ *   SINF, COSF, ACOSF    sin_f / cos_f / acos_f of gd_math.h (glibc 2.35 restated)
+ *   SLERP_SCALE0         (float)(sin((double)w) / (double)sinf(w)): Quaternion::slerp's
+ *                        weight-0 coefficient (ik_bone_segment_3d.cpp:148-151)
+ *   COS_F64_OF_F32       cos((double)x): a cone radius cosine (ik_open_cone_3d.h:47-56)
+ *   COS_F64              cos(x): tangent-radius cosines (ik_open_cone_3d.cpp:36-120) */
+#define MBIK_LIBM_SINF 0
+#define MBIK_LIBM_COSF 1
+#define MBIK_LIBM_ACOSF 2
+#define MBIK_LIBM_SLERP_SCALE0 3
+#define MBIK_LIBM_COS_F64_OF_F32 4
+#define MBIK_LIBM_COS_F64 5
+int32_t mbik_selftest_libm(int32_t fn, uint64_t first, uint64_t count, const double *inputs, const void *expected,
+		uint64_t out[3], void *hip_stream);
+
 const char *mbik_last_error(void);
 
 #ifdef __cplusplus

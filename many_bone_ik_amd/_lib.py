@@ -18,13 +18,16 @@ MBIK_EHIP = -3
 MBIK_EUNSUPPORTED = -4
 MBIK_ENODEV = -5
 
+# mbik_selftest_libm function codes (include/mbik.h)
+LIBM_SINF, LIBM_COSF, LIBM_ACOSF, LIBM_SLERP_SCALE0, LIBM_COS_F64_OF_F32, LIBM_COS_F64 = range(6)
+
 EXPORTED_SYMBOLS = (
     "mbik_plan_create", "mbik_plan_destroy", "mbik_plan_get_info", "mbik_plan_set_launch", "mbik_plan_set_layout",
     "mbik_plan_autotune", "mbik_plan_resident_blocks", "mbik_plan_set_heading_staging",
     "mbik_plan_set_locals_placement", "mbik_plan_set_waves_per_simd", "mbik_plan_rebuild_setup", "mbik_plan_setup_tables",
     "mbik_solve", "mbik_solve_checked", "mbik_solve_host", "mbik_segment_solve", "mbik_plan_segment_table", "mbik_describe_topology",
     "mbik_group_create", "mbik_group_solve", "mbik_group_destroy", "mbik_capture_targets", "mbik_selftest_math",
-    "mbik_last_error",
+    "mbik_selftest_libm", "mbik_last_error",
 )
 
 
@@ -118,6 +121,8 @@ def load():
     L.mbik_solve_checked.restype = C.c_int32
     L.mbik_selftest_math.argtypes = [C.c_int32, C.POINTER(C.c_uint64)]
     L.mbik_selftest_math.restype = C.c_int32
+    L.mbik_selftest_libm.argtypes = [C.c_int32, C.c_uint64, C.c_uint64, vp, vp, C.POINTER(C.c_uint64), vp]
+    L.mbik_selftest_libm.restype = C.c_int32
     L.mbik_solve_host.argtypes = [vp, C.c_int32, C.c_int32, vp, vp, vp]
     L.mbik_solve_host.restype = C.c_int32
     L.mbik_segment_solve.argtypes = [vp, C.c_int32, C.c_int32, C.c_int32, vp, vp, vp]

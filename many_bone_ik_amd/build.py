@@ -1,9 +1,15 @@
 """Builds libmbik.so in-tree for gfx950 (hipcc, no JIT cache, no pip install).
 
-    python -m many_bone_ik_amd.build
+    python -m many_bone_ik_amd.build [--force]
+
+The library is rebuilt whenever the SHA-256 of its inputs -- every source, every header
+under csrc/ and include/, and the compiler flags -- differs from the stamp written next to
+it (libmbik.so.sha256), so an edited header can never leave a stale kernel in place.
 """
 from __future__ import annotations
 
+import glob
+import hashlib
 import os
 import subprocess
 import sys
@@ -12,7 +18,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libmbik.so")
 SOURCES = ["solve.hip", "plan.cpp"]
-HEADERS = ["gd_math.h", "plan.h", os.path.join("..", "..", "include", "mbik.h")]
+STAMP = OUT + ".sha256"
 
 # -ffp-contract=off: every float op rounds separately, as the reference's x86 build does.
 # -fno-slp-vectorize: the SLP vectorizer's packed fp32 ops cost more register copies than
@@ -22,11 +28,26 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp
          "-Wno-unused-result"]
 
 
+def _inputs() -> list[str]:
+    return sorted([os.path.join(CSRC, f) for f in SOURCES] + glob.glob(os.path.join(CSRC, "*.h")) +
+                  glob.glob(os.path.join(HERE, "..", "include", "*.h")), key=os.path.basename)
+
+
+def source_hash(extra_flags=()) -> str:
+    h = hashlib.sha256(" ".join(FLAGS + list(extra_flags)).encode())
+    for f in _inputs():
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
 def _stale() -> bool:
-    if not os.path.exists(OUT):
+    """True unless libmbik.so exists and was built from exactly the current inputs."""
+    if not os.path.exists(OUT) or not os.path.exists(STAMP):
         return True
-    t = os.path.getmtime(OUT)
-    return any(os.path.getmtime(os.path.join(CSRC, f)) > t for f in SOURCES + HEADERS)
+    with open(STAMP) as fh:
+        return fh.read().strip() != source_hash()
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
@@ -36,8 +57,11 @@ def build(force: bool = False, verbose: bool = False) -> str:
     cmd = [hipcc, *FLAGS, *[os.path.join(CSRC, f) for f in SOURCES], "-o", OUT + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
+    digest = source_hash()
     subprocess.run(cmd, check=True)
     os.replace(OUT + ".tmp", OUT)
+    with open(STAMP, "w") as fh:
+        fh.write(digest + "\n")
     return OUT
 
 

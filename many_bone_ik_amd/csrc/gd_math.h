@@ -23,20 +23,6 @@ namespace gd {
 constexpr double CMP_EPSILON = 0.00001;
 constexpr double PI = 3.1415926535897932384626433833;
 
-// Float transcendentals, rounded once from a double evaluation.  The reference calls the
-// platform libm (Math::sin(float) -> sinf); its dynamics amplify 1-ulp libm differences
-// ~2x per iteration, so the product and the oracle pin the same (correctly rounded,
-// barring rare double-rounding cases) result instead of OCML's own float versions.
-#ifdef MBIK_ABLATE_TRIG
-GDI float sin_f(float x) { return sinf(x); }
-GDI float cos_f(float x) { return cosf(x); }
-GDI float acos_f(float x) { return acosf(x); }
-#else
-GDI float sin_f(float x) { return (float)sin((double)x); }
-GDI float cos_f(float x) { return (float)cos((double)x); }
-GDI float acos_f(float x) { return (float)acos((double)x); }
-#endif
-
 // Square root, correctly rounded (IEEE), as Godot's Math::sqrt(float) on x86.
 // On the device: v_rsq_f64 of the widened input and one fp64 Newton correction, rounded
 // once to float.  tools/sqrt_exhaustive.hip checks all 2^32 inputs against the compiler's
@@ -56,6 +42,164 @@ GDI float gd_sqrt(float x) {
 #else
 GDI float gd_sqrt(float x) { return sqrtf(x); }
 #endif
+
+// ---------------- Float transcendentals: the platform libm of the reference ----------------
+// Godot's Math::sin/cos/acos(float) call ::sinf/::cosf/::acosf (core/math/math_funcs.h).  On
+// the reference's Linux x86-64 build that is glibc; the solve amplifies a 1-ulp libm
+// difference ~2x per iteration, so the product reproduces glibc's float
+// results bit for bit on the device and on the host, instead of OCML's own versions.
+// Restated from glibc 2.35 (the image's libm):
+//   sinf/cosf  sysdeps/ieee754/flt-32/s_sinf.c, s_cosf.c, sincosf.h, sincosf_data.c, in the
+//              x86-64 FMA build the ifunc selects on every CPU with FMA (each a*b+c that GCC
+//              contracts there is an explicit fma() here);
+//   acosf      sysdeps/ieee754/flt-32/e_acosf.c (fdlibm, float arithmetic, IEEE sqrt/div).
+// mbik_selftest_libm (tests/test_gpu_libm.py) proves the device results equal to the host
+// libm's on all 2^32 inputs; tools/libm_exhaustive.c does the same for the oracle's copy.
+namespace glibc {
+GDI uint32_t top12(float x) { // exponent and top mantissa bits of |x|
+	union {
+		float f;
+		uint32_t u;
+	} c{x};
+	return (c.u >> 20) & 0x7ffu;
+}
+// the four reduced-argument polynomials' coefficients (sincosf_data.c, first table; the
+// second table is the first with the cosine coefficients negated)
+constexpr double kHalfPiInv24 = 0x1.45F306DC9C883p+23; // 2/pi * 2^24
+constexpr double kHalfPi = 0x1.921FB54442D18p0;
+constexpr double kC0 = 0x1p0, kC1 = -0x1.ffffffd0c621cp-2, kC2 = 0x1.55553e1068f19p-5, kC3 = -0x1.6c087e89a359dp-10,
+				 kC4 = 0x1.99343027bf8c3p-16;
+constexpr double kS1 = -0x1.555545995a603p-3, kS2 = 0x1.1107605230bc4p-7, kS3 = -0x1.994eb3774cf24p-13;
+// sin(x) for the reduced x, x2 = x*x (sinf_poly, even quadrant)
+GDI float sin_poly(double x, double x2) {
+	const double x3 = x * x2;
+	const double s1 = fma(x2, kS3, kS2);
+	const double x7 = x3 * x2;
+	const double s = fma(x3, kS1, x);
+	return (float)fma(x7, s1, s);
+}
+// cos(x) for the reduced x (sinf_poly, odd quadrant, first table)
+GDI float cos_poly(double x2) {
+	const double x4 = x2 * x2;
+	const double c2 = fma(x2, kC4, kC3);
+	const double c1 = fma(x2, kC1, kC0);
+	const double x6 = x4 * x2;
+	const double c = fma(x4, kC2, c1);
+	return (float)fma(x6, c2, c);
+}
+// Payne-Hanek reduction for |y| >= 120 (reduce_large): x * 2^63 / (pi/2) from the bits of
+// 2/pi, in 64-bit integers.  Returns the reduced argument and the quadrant count.
+GDI double reduce_large(uint32_t xi, int &quadrant) {
+	// 2/pi = 0x0.a2f9836e4e441529fc2757d1f534ddc0db629599..., read as 32-bit windows
+	// starting at byte k - 3 (the __inv_pio4 table): window(k) for k = i, i + 4, i + 8.
+	constexpr uint32_t w[24] = {0x000000a2u, 0x0000a2f9u, 0x00a2f983u, 0xa2f9836eu, 0xf9836e4eu, 0x836e4e44u,
+								0x6e4e4415u, 0x4e441529u, 0x441529fcu, 0x1529fc27u, 0x29fc2757u, 0xfc2757d1u,
+								0x2757d1f5u, 0x57d1f534u, 0xd1f534ddu, 0xf534ddc0u, 0x34ddc0dbu, 0xddc0db62u,
+								0xc0db6295u, 0xdb629599u, 0x6295993cu, 0x95993c43u, 0x993c4390u, 0x3c439041u};
+	const int i = (xi >> 26) & 15;
+	const int shift = (xi >> 23) & 7;
+	const uint32_t m = ((xi & 0xffffffu) | 0x800000u) << shift;
+	uint64_t a = (uint64_t)(uint32_t)(m * w[i]); // low 32 bits only, as the C source's 32-bit product
+	const uint64_t b = (uint64_t)m * w[i + 4];
+	const uint64_t c = (uint64_t)m * w[i + 8];
+	a = (c >> 32) | (a << 32);
+	a += b;
+	const uint64_t n = (a + (1ull << 61)) >> 62;
+	a -= n << 62;
+	quadrant = (int)n;
+	return (double)(int64_t)a * 0x1.921FB54442D18p-62;
+}
+// sinf (cos_variant 0) / cosf (cos_variant 1)
+GDI float sincosf(float y, int cos_variant) {
+	const uint32_t t = top12(y);
+	double x = y;
+	if (t < 0x3f4u) { // |y| < 0.75 (abstop12(pi/4))
+		if (t < 0x398u) return cos_variant ? 1.0f : y; // |y| < 2^-12
+		return cos_variant ? cos_poly(x * x) : sin_poly(x, x * x);
+	}
+	int n, ns; // quadrant; quadrant for the sign pattern and table (large inputs add the sign bit)
+	if (t < 0x42fu) { // |y| < 120: reduce_fast
+		const double r = x * kHalfPiInv24;
+		n = ((int32_t)r + 0x800000) >> 24;
+		x = fma(-(double)n, kHalfPi, x);
+		ns = n;
+	} else if (t < 0x7f8u) {
+		union {
+			float f;
+			uint32_t u;
+		} c{y};
+		x = reduce_large(c.u, n);
+		ns = n + (int)(c.u >> 31);
+	} else {
+		return y - y; // inf or NaN -> NaN (__math_invalidf)
+	}
+	// sign of the reduced argument (+, -, -, +) by ns, the sin or cos polynomial by n, the
+	// cosine one negated when ns is in quadrant 2 or 3 (the second table)
+	const double xs = ((ns + 1) & 2) ? -x : x;
+	if (((n ^ cos_variant) & 1) == 0) return sin_poly(xs, xs * xs);
+	const float c = cos_poly(xs * xs);
+	return (ns & 2) ? -c : c;
+}
+// acosf (e_acosf.c)
+GDI float acosf(float x) {
+	constexpr float pi = 3.1415925026e+00f, pio2_hi = 1.5707962513e+00f, pio2_lo = 7.5497894159e-08f;
+	constexpr float pS0 = 1.6666667163e-01f, pS1 = -3.2556581497e-01f, pS2 = 2.0121252537e-01f, pS3 = -4.0055535734e-02f,
+					pS4 = 7.9153501429e-04f, pS5 = 3.4793309169e-05f;
+	constexpr float qS1 = -2.4033949375e+00f, qS2 = 2.0209457874e+00f, qS3 = -6.8828397989e-01f, qS4 = 7.7038154006e-02f;
+	union {
+		float f;
+		int32_t i;
+	} c{x};
+	const int32_t hx = c.i, ix = hx & 0x7fffffff;
+	if (ix >= 0x3f800000) { // |x| >= 1
+		if (ix == 0x3f800000) return hx > 0 ? 0.0f : pi + 2.0f * pio2_lo;
+		return (x - x) / (x - x);
+	}
+	auto rat = [&](float z) {
+		const float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+		const float q = 1.0f + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+		return p / q;
+	};
+	if (ix < 0x3f000000) { // |x| < 0.5
+		if (ix <= 0x32800000) return pio2_hi + pio2_lo;
+		const float r = rat(x * x);
+		return pio2_hi - (x - (pio2_lo - x * r));
+	}
+	if (hx < 0) { // x <= -0.5
+		const float z = (1.0f + x) * 0.5f;
+		const float s = gd_sqrt(z);
+		const float r = rat(z);
+		const float w = r * s - pio2_lo;
+		return pi - 2.0f * (s + w);
+	}
+	const float z = (1.0f - x) * 0.5f; // x >= 0.5
+	const float s = gd_sqrt(z);
+	union {
+		float f;
+		uint32_t u;
+	} d{s};
+	d.u &= 0xfffff000u;
+	const float df = d.f;
+	const float cc = (z - df * df) / (s + df);
+	const float r = rat(z);
+	const float w = r * s + cc;
+	return 2.0f * (df + w);
+}
+} // namespace glibc
+
+GDI float sin_f(float x) { return glibc::sincosf(x, 0); }
+GDI float cos_f(float x) { return glibc::sincosf(x, 1); }
+GDI float acos_f(float x) { return glibc::acosf(x); }
+// Quaternion::slerp's coefficient of the start quaternion at weight 0 (Godot 4.3
+// quaternion.cpp, reached from Basis::slerp at ik_bone_segment_3d.cpp:148-151):
+// scale0 = Math::sin((1.0 - p_weight) * omega) / sinom, the numerator a double ::sin, the
+// denominator sinom = Math::sin(omega) a float sinf.  (scale1 = sinf(0 * omega) / sinom = +0.)
+// The double sin is the device's own (OCML); mbik_selftest_libm proves this quotient equal
+// to the host glibc's for every float omega.
+GDI float slerp_scale0(float omega) {
+	const float sinom = sin_f(omega);
+	return (float)(sin((double)omega) / (double)sinom);
+}
 
 struct V3 {
 	float x, y, z;

@@ -13,9 +13,11 @@
 //  * a skeleton's local poses L and iteration-start globals G live in LDS; targets too;
 //  * sibling segments (equal height in the segment tree) run concurrently on disjoint
 //    aligned lane groups; within a segment, effectors (and their headings) are spread over
-//    the group's lanes and the QCP sums are reduced with cross-lane xor shuffles (fp64,
-//    as the reference accumulates), after which every lane of the group runs the scalar
-//    rotation / constraint chain redundantly (bitwise identical) -- no broadcast needed;
+//    the group's lanes, which stage their QCP terms in LDS; each fp64 QCP sum is then
+//    accumulated by one lane in the reference's heading order (never a shuffle tree: that
+//    would change the rounding) and exchanged through LDS, after which every lane of the
+//    group runs the scalar rotation / constraint chain redundantly (bitwise identical) -- no
+//    broadcast needed;
 //  * per-skeleton plan tables (bone directions, cones, twist frames) are SoA in HBM,
 //    [item][field][skeleton], read as the solve reaches them.
 // The kernel is built with -ffp-contract=off so every float operation rounds as the
@@ -203,12 +205,8 @@ __device__ __forceinline__ B3 slerp_weight0(const B3 &from_b, const SlerpTo &tt)
 	}
 	float scale0, scale1;
 	if ((1.0f - cosom) > (float)CMP_EPSILON) {
-		float omega = acos_f(cosom);
-		// sinom = sinf(omega) and scale0 = sin((1.0 - 0) * omega) / sinom share one double
-		// evaluation; scale1 = sinf(0 * omega) / sinom is +0 for the finite omega of this branch.
-		double so = sin((double)omega);
-		float sinom = (float)so;
-		scale0 = (float)(so / (double)sinom);
+		// scale1 = sinf(0 * omega) / sinom is +0 for the finite omega of this branch
+		scale0 = slerp_scale0(acos_f(cosom));
 		scale1 = 0.0f;
 	} else {
 		scale0 = 1.0f;
@@ -1979,6 +1977,55 @@ __global__ void mbik_selftest_math_kernel(unsigned long long *out) {
 	if (bad) atomicAdd(&out[0], bad);
 	if (nan_bad) atomicAdd(&out[1], nan_bad);
 }
+// mbik_selftest_libm: the device's transcendental call sites against host-computed values.
+// out[0] = observable mismatches, out[1] = lowest such index (atomicMin; ~0 if none),
+// out[2] = results whose bits differ at all.
+template <class T>
+__device__ __forceinline__ bool same_bits(T a, T b) {
+	if (a != a && b != b) return true; // NaN payloads aside
+	return a == b && (a != 0 || signbit(a) == signbit(b));
+}
+// Two double results the solve cannot tell apart: the setup's double cosines are only
+// compared with float-valued doubles (ik_open_cone_3d.cpp:358-381, :285-321) or rounded to
+// float (:36-120), so they are equivalent when no float lies in [lo, hi) ... (lo, hi] and
+// both round to the same float (a comparison d > c, d a float, then resolves alike).
+__device__ __forceinline__ bool same_for_float_use(double a, double b) {
+	if (same_bits(a, b)) return true;
+	if (a != a || b != b) return false;
+	const double lo = a < b ? a : b, hi = a < b ? b : a;
+	if ((float)lo != (float)hi) return false;
+	return !((double)__double2float_rd(hi) > lo); // no float f with lo < f <= hi
+}
+__global__ void mbik_selftest_libm_kernel(int fn, uint64_t first, uint64_t count, const double *__restrict__ inputs,
+		const void *__restrict__ expected, unsigned long long *out) {
+	const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
+	unsigned long long bad = 0, lo = ~0ull, diff = 0;
+	for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += nthreads) {
+		const float x = __uint_as_float((unsigned)(first + i));
+		bool ok, exact;
+		if (fn <= MBIK_LIBM_SLERP_SCALE0) {
+			const float e = static_cast<const float *>(expected)[i];
+			const float g = fn == MBIK_LIBM_SINF ? sin_f(x) : fn == MBIK_LIBM_COSF ? cos_f(x) : fn == MBIK_LIBM_ACOSF ? acos_f(x)
+																							: slerp_scale0(x);
+			ok = exact = same_bits(e, g);
+		} else {
+			const double e = static_cast<const double *>(expected)[i];
+			const double g = fn == MBIK_LIBM_COS_F64_OF_F32 ? ::cos((double)x) : ::cos(inputs[i]);
+			exact = same_bits(e, g);
+			ok = same_for_float_use(e, g);
+		}
+		diff += !exact;
+		if (!ok) {
+			bad++;
+			lo = i < lo ? i : lo;
+		}
+	}
+	if (bad) {
+		atomicAdd(&out[0], bad);
+		atomicMin(&out[1], lo);
+	}
+	if (diff) atomicAdd(&out[2], diff);
+}
 } // namespace
 extern "C" {
 
@@ -2001,6 +2048,34 @@ int32_t mbik_selftest_math(int32_t device, uint64_t out[2]) {
 	(void)hipFree(d);
 	out[0] = h[0];
 	out[1] = h[1];
+	return rc;
+}
+
+int32_t mbik_selftest_libm(int32_t fn, uint64_t first, uint64_t count, const double *inputs, const void *expected,
+		uint64_t out[3], void *hip_stream) {
+	if (!out || !expected) return fail(MBIK_EINVAL, "null argument");
+	if (fn < MBIK_LIBM_SINF || fn > MBIK_LIBM_COS_F64) return fail(MBIK_EINVAL, "unknown function code");
+	if (fn == MBIK_LIBM_COS_F64 ? !inputs : first + count > (1ull << 32)) return fail(MBIK_EINVAL, "input range");
+	out[0] = 0;
+	out[1] = ~0ull;
+	out[2] = 0;
+	if (count == 0) return MBIK_OK;
+	hipStream_t st = reinterpret_cast<hipStream_t>(hip_stream);
+	unsigned long long *d = nullptr;
+	if (hipMalloc(&d, 3 * sizeof(unsigned long long)) != hipSuccess) return fail(MBIK_ENOMEM, "hipMalloc");
+	unsigned long long h[3] = {0, ~0ull, 0};
+	int rc = MBIK_OK;
+	if (hipMemcpyAsync(d, h, sizeof(h), hipMemcpyHostToDevice, st) != hipSuccess) rc = fail(MBIK_EHIP, "hipMemcpyAsync");
+	if (rc == MBIK_OK) {
+		hipLaunchKernelGGL(mbik_selftest_libm_kernel, dim3(4096), dim3(256), 0, st, (int)fn, first, count, inputs, expected, d);
+		if (hipGetLastError() != hipSuccess) rc = fail(MBIK_EHIP, "self-test launch");
+	}
+	if (rc == MBIK_OK && hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, st) != hipSuccess) rc = fail(MBIK_EHIP, "hipMemcpyAsync");
+	if (rc == MBIK_OK && hipStreamSynchronize(st) != hipSuccess) rc = fail(MBIK_EHIP, "self-test kernel");
+	(void)hipFree(d);
+	out[0] = h[0];
+	out[1] = h[1];
+	out[2] = h[2];
 	return rc;
 }
 

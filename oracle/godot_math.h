@@ -31,20 +31,29 @@
 #define GD_TAU 6.2831853071795864769252867666
 
 /* Float transcendentals.  Godot's Math::sin/cos/acos(float) call the platform libm
- * (sinf/cosf/acosf), whose last-ulp behaviour differs between libms (glibc, MSVC, ...).
- * The reference's dynamics amplify a 1-ulp difference ~2x per iteration, so the oracle
- * pins the rounding: by default each is evaluated in double and rounded once (correctly
- * rounded except in rare double-rounding cases), which the GPU path reproduces.  Build
- * with -DORACLE_PLATFORM_LIBM to call the platform libm instead (DESIGN.md quantifies the
- * spread between the two). */
-#ifdef ORACLE_PLATFORM_LIBM
-static inline float gd_sinf(float x) { return sinf(x); }
-static inline float gd_cosf(float x) { return cosf(x); }
-static inline float gd_acosf(float x) { return acosf(x); }
-#else
+ * (::sinf/::cosf/::acosf, core/math/math_funcs.h); Math::sin(double) calls ::sin.  The
+ * reference's dynamics amplify a 1-ulp difference ~2x per iteration, so the libm is part
+ * of the reference's behaviour.  The oracle calls the platform libm, as a Linux x86-64
+ * Godot build does: glibc 2.35 here and on the GPU boxes (same image).  glibc_libm.h
+ * restates its sinf/cosf/acosf and tools/libm_exhaustive.c shows the two equal on all
+ * 2^32 inputs (FMA ifunc variant; profiles/r02_libm_exhaustive.txt).  Two study builds:
+ *   -DORACLE_GLIBC_RESTATED  the restatement instead of the platform libm (a host whose
+ *                            libm is not glibc 2.35 still gets the reference's rounding);
+ *   -DORACLE_PINNED_TRIG     round-1's convention, (float)f((double)x), for
+ *                            tools/libm_sensitivity.py only. */
+#if defined(ORACLE_PINNED_TRIG)
 static inline float gd_sinf(float x) { return (float)sin((double)x); }
 static inline float gd_cosf(float x) { return (float)cos((double)x); }
 static inline float gd_acosf(float x) { return (float)acos((double)x); }
+#elif defined(ORACLE_GLIBC_RESTATED)
+#include "glibc_libm.h"
+static inline float gd_sinf(float x) { return glibc_sinf(x); }
+static inline float gd_cosf(float x) { return glibc_cosf(x); }
+static inline float gd_acosf(float x) { return glibc_acosf(x); }
+#else
+static inline float gd_sinf(float x) { return sinf(x); }
+static inline float gd_cosf(float x) { return cosf(x); }
+static inline float gd_acosf(float x) { return acosf(x); }
 #endif
 
 typedef struct { float x, y, z; } v3;

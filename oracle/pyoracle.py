@@ -66,6 +66,11 @@ def lib():
         L.oracle_xform_affine_inverse.argtypes = [_f32p, _f32p]
         L.oracle_basis_to_quat.argtypes = [_f32p, _f32p]
         L.oracle_quat_to_basis.argtypes = [_f32p, _f32p]
+        L.oracle_libm_fill.argtypes = [C.c_int32, C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p, C.c_int32]
+        L.oracle_libm_fill.restype = C.c_int32
+        L.oracle_libm_restated_mismatches.argtypes = [C.c_int32, C.c_uint64, C.c_uint64, C.c_uint64,
+                                                      C.POINTER(C.c_uint64)]
+        L.oracle_libm_restated_mismatches.restype = C.c_uint64
         _lib = L
     return _lib
 
@@ -213,3 +218,22 @@ def xform_affine_inverse(a):
     out = np.zeros(12, np.float32)
     lib().oracle_xform_affine_inverse(np.ascontiguousarray(a, np.float32), out)
     return out
+
+
+def libm_fill(fn: int, first: int, count: int, inputs: np.ndarray | None = None, threads: int = 8) -> np.ndarray:
+    """Host platform-libm values of the device's transcendental call sites (libm_ref.c):
+    float results for codes 0-3, double for 4-5 (codes as MBIK_LIBM_* in include/mbik.h)."""
+    out = np.empty(count, np.float32 if fn <= 3 else np.float64)
+    if inputs is not None:
+        inputs = np.ascontiguousarray(inputs, np.float64)
+    rc = lib().oracle_libm_fill(fn, first, count, _ptr(inputs), out.ctypes.data, threads)
+    assert rc == 0
+    return out
+
+
+def libm_restated_mismatches(fn: int, first: int, count: int, stride: int = 1):
+    """glibc_libm.h vs the platform libm (codes 0-2) on `count` inputs first, first+stride, ...:
+    (mismatches, first mismatching bit pattern or None)."""
+    fb = C.c_uint64(0)
+    n = int(lib().oracle_libm_restated_mismatches(fn, first, count, stride, C.byref(fb)))
+    return n, (int(fb.value) if n else None)

@@ -5,8 +5,9 @@
 Each fixture stores the generator coordinates (config, first skeleton, count), a SHA-256
 of the generated inputs (so generator drift is caught), and the oracle's outputs:
 full-frame poses, and for C1 (the reference's own CPU case) the pose after every
-iteration.  The oracle is the plain-C restatement in oracle/ (transcendentals pinned to
-correctly rounded evaluation, see oracle/godot_math.h).
+iteration.  The oracle is the plain-C restatement in oracle/; its transcendentals are the
+platform libm's, glibc 2.35 (x86-64 FMA ifunc variant) -- what a Linux x86-64 Godot build
+of the reference calls (oracle/godot_math.h; the 'libm' key records it).
 """
 from __future__ import annotations
 
@@ -23,6 +24,7 @@ sys.path.insert(0, ROOT)
 from many_bone_ik_amd import workloads as W  # noqa: E402
 from oracle import pyoracle as po  # noqa: E402
 
+LIBM = "glibc 2.35 platform libm (sinf/cosf/acosf FMA ifunc variant; tools/libm_exhaustive.c)"
 FIXTURES = [(1, 0, 1), (2, 0, 4), (3, 0, 4), (4, 0, 2), (5, 0, 1), (2, 4093, 3)]
 
 
@@ -44,7 +46,7 @@ def main():
         name = os.path.join(HERE, f"oracle_c{cfg}_{first}_{n}.npz")
         np.savez_compressed(name, cfg=cfg, first=first, n=n, digest=input_digest(wl), pose_out=out,
                             trace=trace if cfg == 1 else trace[:, :1], seg_root=seg_root, seg_tip=seg_tip,
-                            seg_nh=seg_nh, bone_list=np.array(o.bone_list(), np.int32), segment0_pose=seg0)
+                            seg_nh=seg_nh, libm=LIBM, bone_list=np.array(o.bone_list(), np.int32), segment0_pose=seg0)
         print(name, os.path.getsize(name), "bytes")
 
 

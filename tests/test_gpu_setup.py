@@ -1,6 +1,12 @@
 """GPU plan setup (mbik_plan_rebuild_setup): the per-skeleton bone-direction
-and Kusudama frames derived on the device equal the host builder's tables bitwise, and solves
-after a rebuild stay bitwise equal to the oracle.  Needs an MI355X: -m gpu."""
+and Kusudama frames derived on the device equal the host builder's tables, and solves after a
+rebuild stay bitwise equal to the oracle.  Needs an MI355X: -m gpu.
+
+D and CF (floats) must be bitwise equal.  CD holds double cosines of the cone and tangent
+radii: the host evaluates them with glibc's cos (the reference's), the device with its own,
+and the two differ in the last bit for ~1.6 % of inputs (tests/test_gpu_libm.py).  The solve
+only compares CD entries with float-valued doubles (ik_open_cone_3d.cpp:285-321, :358-381), so
+CD must be *observably* equal: the same bits, or adjacent doubles with no float between them."""
 import math
 
 import numpy as np
@@ -18,11 +24,26 @@ def _dev(torch, a):
     return torch.from_numpy(np.ascontiguousarray(a)).to(torch.device("cuda", 0))
 
 
+def _float_between(lo, hi):
+    """Is there a float f with lo < f <= hi (elementwise, lo <= hi)?"""
+    f = hi.astype(np.float32)
+    f = np.where(f.astype(np.float64) > hi, np.nextafter(f, np.float32(-np.inf)), f)
+    return f.astype(np.float64) > lo
+
+
 def _assert_tables_equal(a, b, what):
     for name, x, y in zip(("D", "CF", "CD"), a, b):
         assert x.shape == y.shape, (what, name)
         bad = np.argwhere(x.view(np.uint32 if x.dtype == np.float32 else np.uint64)
                           != y.view(np.uint32 if y.dtype == np.float32 else np.uint64))
+        if name == "CD" and bad.size:
+            xs, ys = x[tuple(bad.T)], y[tuple(bad.T)]
+            lo, hi = np.minimum(xs, ys), np.maximum(xs, ys)
+            ulps = np.abs(xs.view(np.int64) - ys.view(np.int64))
+            assert (ulps <= 1).all() and not _float_between(lo, hi).any() and \
+                np.array_equal(lo.astype(np.float32), hi.astype(np.float32)), \
+                f"{what} CD: {len(bad)} entries differ observably"
+            continue
         assert bad.size == 0, f"{what} {name}: {len(bad)} entries differ, first {bad[:4].tolist()}"
 
 
@@ -45,6 +66,23 @@ def test_gpu_setup_equals_host_setup(mbik, name, topo):
     pose, cones, twist = _dev(torch, wl.pose), _dev(torch, wl.cones), _dev(torch, wl.twist)
     plan.rebuild_setup(pose.data_ptr(), cones.data_ptr(), twist.data_ptr(), stream=torch.cuda.current_stream().cuda_stream)
     _assert_tables_equal(plan.setup_tables(), host, name)
+
+
+def test_gpu_setup_random_radii(oracle, mbik):
+    """Per-skeleton random cone radii and twist ranges (every cosine a different input):
+    tables observably equal, and the solve after the GPU rebuild bitwise equal to the oracle."""
+    import torch
+    wl = W.generate(2, 128, first=31)
+    rng = np.random.default_rng(7)
+    wl.cones[..., 3] = rng.uniform(0.05, 1.2, wl.cones.shape[:-1]).astype(np.float32)
+    wl.twist[..., 1] = rng.uniform(0.1, 6.0, wl.twist.shape[:-1]).astype(np.float32)
+    plan = Plan.from_workload(wl)
+    host = plan.setup_tables()
+    pose, cones, twist = _dev(torch, wl.pose), _dev(torch, wl.cones), _dev(torch, wl.twist)
+    plan.rebuild_setup(pose.data_ptr(), cones.data_ptr(), twist.data_ptr(), stream=torch.cuda.current_stream().cuda_stream)
+    _assert_tables_equal(plan.setup_tables(), host, "random radii")
+    ref = oracle.Oracle(wl).solve(wl.pose, wl.targets, threads=8)
+    assert_parity(plan.solve_host(wl.pose, wl.targets), ref, "solve after GPU setup, random radii")
 
 
 def test_gpu_setup_from_new_poses_matches_a_fresh_plan(oracle, mbik):
@@ -75,4 +113,4 @@ def test_gpu_setup_partial_range(mbik):
     fresh = Plan.from_workload(b).setup_tables()
     for x, y, z in zip(before, after, fresh):
         assert np.array_equal(x[..., :10], y[..., :10]) and np.array_equal(x[..., 20:], y[..., 20:])
-        assert np.array_equal(y[..., 10:20].view(np.uint8), z[..., 10:20].view(np.uint8))
+    _assert_tables_equal([y[..., 10:20] for y in after], [z[..., 10:20] for z in fresh], "partial range")
