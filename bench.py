@@ -5,10 +5,19 @@
 
 One *step* = one mbik_solve() over this rank's batch of skeletons (BASELINE.json
 configs[1] = C2 by default: 4096 x 32 bones / 4 effectors / 2 Kusudama cones per bone,
-16 iterations), inputs already resident in HBM.  N > 1 is launched by
-torch.distributed.run, one rank per GPU; every rank solves its own shard of skeletons
-(weak scaling, no collective on the data path) and an RCCL all_gather of the output poses
-is timed separately after the solve loop ("gather_ms").  Rank 0 prints one JSON line.
+16 iterations), inputs already resident in HBM.  Rank 0 prints one JSON line.
+
+N > 1 runs one rank per GPU.  Under torch.distributed.run (WORLD_SIZE set) this process is
+a rank; WORLD_SIZE must equal --gpus.  Run as a plain command with --gpus N > 1, it starts
+torch.distributed.run itself as a child process (before anything touches the GPU) and exits
+with its status.  Every rank solves its own contiguous shard of skeletons with no
+collective on the data path:
+  --scaling weak    (default) the config's skeletons_per_gpu on every rank;
+  --scaling strong  the config's whole batch (C4: 262,144) split by dist.shard_range.
+The RCCL gathers of the output poses are timed separately after the solve loop.
+
+--dry-run exercises the launcher / rendezvous / sharding / timing plumbing on CPU (gloo,
+no GPU, no solve): the tests use it, its line says "dry_run": true and is never a result.
 """
 from __future__ import annotations
 
@@ -26,7 +35,8 @@ sys.path.insert(0, HERE)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
 VALU_PEAK_TFLOPS = 157.3  # MI355X FP32 vector peak (same guide)
-SKEL_PER_GPU = {2: 4096, 3: 65536, 4: 262144 // 8, 5: 16384}
+SKEL_PER_GPU = {2: 4096, 3: 65536, 4: 262144 // 8, 5: 16384}      # weak scaling
+SKEL_TOTAL = {2: 4096, 3: 65536, 4: 262144, 5: 16384}             # strong scaling (BASELINE configs)
 METRIC = "skeletons/sec to convergence (32-bone/4-eff, 16 iters) at 1/2/4/8 GPU; bone-quat max-err vs ref"
 
 
@@ -36,7 +46,11 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5])
-    ap.add_argument("--skeletons", type=int, default=0, help="skeletons per GPU (default: the config's)")
+    ap.add_argument("--skeletons", type=int, default=0,
+                    help="skeletons per GPU (weak) or in total (strong); default: the config's")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU-only plumbing check: gloo, no GPU, no solve (tests)")
     ap.add_argument("--lanes", type=int, default=0, help="lanes per skeleton override (0 = plan default)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -50,12 +64,35 @@ def parse():
     return ap.parse_args()
 
 
+def host_cpu() -> dict:
+    """The host cores this process may run on: affinity (what `nproc` prints), the cgroup CPU
+    quota if one is set, os.cpu_count() (the whole machine) and the CPU model."""
+    info = {"nproc": len(os.sched_getaffinity(0)), "cpu_count": os.cpu_count(), "cgroup_quota_cpus": None,
+            "cpu_model": None}
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            info["cgroup_quota_cpus"] = int(q) / int(p)
+    except (OSError, ValueError):
+        pass
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                info["cpu_model"] = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return info
+
+
 def cpu_baseline(cfg: int, seconds: float, **flags):
-    """Oracle (plain-C restatement of the reference) on the host cores, bounded sample."""
+    """Oracle (plain-C restatement of the reference) on every host core this process may use
+    (`nproc` threads), bounded sample of the same workload."""
     from many_bone_ik_amd import workloads as W
     from oracle import pyoracle as po
-    threads = max(1, min(16, os.cpu_count() or 1))
-    n = 512 if cfg in (2, 3, 4) else 64
+    hc = host_cpu()
+    threads = hc["nproc"]
+    n = max(512, 8 * threads) if cfg in (2, 3, 4) else max(64, 2 * threads)
     wl = W.generate(cfg, n)
     o = po.Oracle(wl, **flags)
     done = 0
@@ -68,34 +105,54 @@ def cpu_baseline(cfg: int, seconds: float, **flags):
             break
     o.close()
     return {"value": done / el, "unit": "skeletons/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/ (C restatement of the reference solve, reference object model) on config C{cfg}: "
-                      f"{n} skeletons solved {done // n} times in {el:.1f} s with {threads} threads"}
+            "sample": f"oracle/ (C restatement of the reference solve, platform libm) on config C{cfg}: "
+                      f"{n} skeletons solved {done // n} times in {el:.1f} s with {threads} threads",
+            **hc}
+
+
+def launch_ranks(args) -> int:
+    """`bench.py --gpus N` (N > 1) run as a plain command: start torch.distributed.run with N
+    ranks as a child process and return its exit status (non-zero if any rank failed).  This
+    parent never imports torch or touches the GPU."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
 
 
 def main():
     args = parse()
+    if args.gpus < 1:
+        sys.exit("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and world > 1:
-        print(f"warning: WORLD_SIZE={world} != --gpus {args.gpus}", file=sys.stderr)
+    if world != args.gpus:
+        sys.exit(f"WORLD_SIZE={world} but --gpus {args.gpus}: one rank per GPU is required")
+    if args.dry_run:
+        return dry_run(args, world, rank)
     dist = None
+    torch.cuda.set_device(local_rank)
     if world > 1:
         import torch.distributed as dist_mod
         dist = dist_mod
-        torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    else:
-        torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
 
     from many_bone_ik_amd import workloads as W
+    from many_bone_ik_amd.dist import gather_poses, gather_poses_to_root
     from many_bone_ik_amd.solver import Plan, quat_error
 
     cfg = args.config
-    n = args.skeletons or SKEL_PER_GPU[cfg]
-    first = rank * n
+    total, first, n = batch_shard(args, world, rank)
     wl = W.generate(cfg, n, first=first)
     flags = dict(constraint_mode=args.constraint_mode, stabilization_passes=args.stabilization_passes)
     plan = Plan.from_workload(wl, device=local_rank, lanes=args.lanes, **flags)
@@ -139,11 +196,10 @@ def main():
 
     gather_ms = gather_root_ms = None
     if dist:
-        parts = [torch.empty_like(pose_out) for _ in range(world)]
         dist.barrier()
         torch.cuda.synchronize(dev)
         g0 = time.perf_counter()
-        dist.all_gather(parts, pose_out)
+        gather_poses(pose_out, total)
         torch.cuda.synchronize(dev)
         gt = torch.tensor([time.perf_counter() - g0], dtype=torch.float64, device=dev)
         dist.all_reduce(gt, op=dist.ReduceOp.MAX)
@@ -151,11 +207,10 @@ def main():
         # SURVEY §8(e)'s variant: every rank sends its shard to rank 0 only (one xGMI link
         # each).  Reported beside the solve, never part of `value`; a failure is reported too.
         try:
-            from many_bone_ik_amd.dist import gather_poses_to_root
             dist.barrier()
             torch.cuda.synchronize(dev)
             g0 = time.perf_counter()
-            gather_poses_to_root(pose_out, n * world, root=0)
+            gather_poses_to_root(pose_out, total, root=0)
             torch.cuda.synchronize(dev)
             gt = torch.tensor([time.perf_counter() - g0], dtype=torch.float64, device=dev)
             dist.all_reduce(gt, op=dist.ReduceOp.MAX)
@@ -183,7 +238,7 @@ def main():
             k = min(64, n)
             sub = W.generate(cfg, k, first=first)
             o = po.Oracle(sub, **flags)
-            ref = o.solve(sub.pose, sub.targets, threads=max(1, min(16, os.cpu_count() or 1)))
+            ref = o.solve(sub.pose, sub.targets, threads=len(os.sched_getaffinity(0)))
             if args.constraint_mode:  # frames advance the node caches: compare a fresh first frame
                 sp = Plan.from_workload(sub, device=local_rank, **flags)
                 got = sp.solve_host(sub.pose, sub.targets)
@@ -201,7 +256,6 @@ def main():
         if dist:
             dist.destroy_process_group()
         return
-    total = n * world
     ms_per_step = wall_max / args.steps * 1e3
     value = total / (wall_max / args.steps)
     alg_bytes = info["algorithmic_bytes_per_skeleton"] * n
@@ -239,14 +293,14 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (seeded generator, many_bone_ik_amd/workloads.py)",
         "config": {"workload": W.bench_config_name(cfg) + (" + constraint_mode" if args.constraint_mode else "") +
                                (f" + stabilization_passes={args.stabilization_passes}" if args.stabilization_passes else ""),
                    "baseline_config": f"configs[{cfg - 1}]",
-                   "skeletons_per_gpu": n, "bones": wl.bone_count, "effectors": int(wl.topo.pins.shape[0]),
+                   "skeletons_total": total, "skeletons_per_gpu": n, "bones": wl.bone_count, "effectors": int(wl.topo.pins.shape[0]),
                    "cones_per_bone": wl.topo.cones_per_bone, "iterations": wl.topo.iterations,
                    "lanes_per_skeleton": info["lanes_per_skeleton"], "skeletons_per_block": info["skeletons_per_block"],
                    "lds_bytes_per_block": info["lds_bytes_per_block"],
@@ -274,6 +328,48 @@ def main():
             out["cpu_baseline"] = {"error": str(e)}
     print(json.dumps(out))
     if dist:
+        dist.destroy_process_group()
+
+
+def batch_shard(args, world: int, rank: int):
+    """(total skeletons, this rank's first, this rank's count) for --scaling."""
+    from many_bone_ik_amd.dist import shard_range
+    if args.scaling == "weak":
+        per = args.skeletons or SKEL_PER_GPU[args.config]
+        return per * world, rank * per, per
+    total = args.skeletons or SKEL_TOTAL[args.config]
+    first, count = shard_range(rank, world, total)
+    return total, first, count
+
+
+def dry_run(args, world: int, rank: int):
+    """The multi-rank plumbing without a GPU: gloo rendezvous, this rank's shard, barrier +
+    max-over-ranks timing of no-op steps, the pose gather, and rank 0's JSON line."""
+    import torch
+    import torch.distributed as dist
+    from many_bone_ik_amd.dist import gather_poses
+    if world > 1:
+        dist.init_process_group("gloo")
+    total, first, n = batch_shard(args, world, rank)
+    shard = torch.arange(first, first + n, dtype=torch.float32).reshape(n, 1, 1).expand(n, 1, 10).contiguous()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pass
+    if world > 1:
+        dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    full = gather_poses(shard, total) if world > 1 else shard
+    ok = bool(torch.equal(full[:, 0, 0], torch.arange(total, dtype=torch.float32)))
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "skeletons/s", "n_gpus": world,
+                          "steps": args.steps, "warmup": args.warmup, "scaling": args.scaling, "dry_run": True,
+                          "config": {"skeletons_total": total, "skeletons_per_gpu": n},
+                          "gathered_in_order": ok, "max_wall_s": float(el.item())}))
+    if world > 1:
         dist.destroy_process_group()
 
 

@@ -50,7 +50,7 @@ extern "C" {
 #define MBIK_EUNSUPPORTED (-4)
 #define MBIK_ENODEV (-5)
 
-#define MBIK_ABI_VERSION 2
+#define MBIK_ABI_VERSION 3
 
 typedef struct mbik_plan mbik_plan;
 typedef struct mbik_group mbik_group;
@@ -108,6 +108,9 @@ typedef struct mbik_plan_info {
 	int32_t heading_staging;           /* mbik_plan_set_heading_staging in effect (0 / 1) */
 	int32_t state_placement;           /* mbik_plan_set_locals_placement in effect (0 / 1 / 2) */
 	int32_t waves_per_simd;            /* mbik_plan_set_waves_per_simd in effect (1 / 2) */
+	int32_t constraint_slots;          /* slots of mbik_plan_setup_tables' CF / CD (ABI 3) */
+	int32_t cf_stride;                 /* floats per slot of CF = 14 + 31*max_cones (ABI 3) */
+	int32_t cd_stride;                 /* doubles per slot of CD = 2*max_cones (ABI 3) */
 } mbik_plan_info;
 
 /* Builds the per-topology tables and the per-skeleton setup data for skeletons
@@ -152,8 +155,9 @@ int32_t mbik_plan_set_waves_per_simd(mbik_plan *plan, int32_t waves);
 int32_t mbik_plan_rebuild_setup(mbik_plan *plan, int32_t first, int32_t count, const float *setup_pose,
 		const float *cones, const float *twist, void *hip_stream);
 /* Copies the plan's per-skeleton setup tables to host buffers (any may be NULL):
- * D [bones][9][n], CF [slots][14 + 13*max_cones][n] floats, CD [slots][2*max_cones][n]
- * doubles, n = skeleton_count; slots = constraints on bones in the IK bone list. */
+ * D [bones][9][n], CF [slots][14 + 31*max_cones][n] floats, CD [slots][2*max_cones][n]
+ * doubles, n = skeleton_count; slots = constraints on bones in the IK bone list
+ * (mbik_plan_info.constraint_slots; the strides are mbik_plan_info.cf_stride / cd_stride). */
 int32_t mbik_plan_setup_tables(const mbik_plan *plan, float *D, float *CF, double *CD);
 /* Diagnostic: how many one-wave blocks using lds_bytes_per_block of LDS one CU of the plan's
  * device holds at once (the runtime occupancy query for the plan's kernel). */
@@ -163,7 +167,8 @@ int32_t mbik_plan_resident_blocks(const mbik_plan *plan, int64_t lds_bytes_per_b
  * interval, heading staging, state placement and waves per SIMD; dimensions pinned by the
  * setters above (a value other than 0 / -1) are kept.  A launch that is fully resident at the
  * default layout is left as it is (one skeleton's chain bounds it).  Runs the solve several
- * times into pose_out (identical results); synchronizes hip_stream.  The chosen layout is
+ * times from pose_in into pose_out (identical results); the two buffers must not overlap
+ * (MBIK_EINVAL otherwise).  Synchronizes hip_stream.  The chosen layout is
  * fixed afterwards; mbik_plan_set_layout(plan, 0, 0, 0) and the staging / placement / waves
  * setters with -1 return to the defaults. */
 int32_t mbik_plan_autotune(mbik_plan *plan, int32_t first, int32_t count, const float *pose_in, const float *targets,
@@ -171,7 +176,18 @@ int32_t mbik_plan_autotune(mbik_plan *plan, int32_t first, int32_t count, const 
 
 /* One frame for skeletons [first, first+count): device pointers (hipMalloc'd, on the
  * plan's device), asynchronous on hip_stream (NULL = default stream).  pose_in, targets
- * and pose_out are indexed from skeleton `first`. */
+ * and pose_out are indexed from skeleton `first`; pose_out may equal pose_in (in place).
+ *
+ * Size limits (MBIK_EUNSUPPORTED, from mbik_plan_create or the first solve):
+ *   - an effector's path from the root may hold at most MBIK_MAX_PATH_BONES bones;
+ *   - the LDS of one launch block, mbik_plan_info.lds_bytes_per_block = the topology tables
+ *     plus the solve state of its skeletons (state placement 0 keeps ~12 floats per bone and
+ *     ~25 per pin per skeleton there, placement 2 none), must fit MBIK_MAX_LDS_BYTES; the
+ *     automatic layout shrinks skeletons per block and moves state to device memory first,
+ *     so only the topology tables of a very large rig (several thousand bones) hit this;
+ *   - constraint_mode stages its per-lane stacks in LDS with the same limit. */
+#define MBIK_MAX_PATH_BONES 4096
+#define MBIK_MAX_LDS_BYTES (160 * 1024)
 int32_t mbik_solve(mbik_plan *plan, int32_t first, int32_t count, const float *pose_in, const float *targets,
 		float *pose_out, void *hip_stream);
 /* mbik_solve plus a per-skeleton status byte (device buffer of `count` bytes, indexed from

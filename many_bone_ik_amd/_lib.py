@@ -61,7 +61,8 @@ class MbikPlanInfo(C.Structure):
                 ("algorithmic_bytes_per_skeleton", C.c_double),
                 ("algorithmic_flops_per_skeleton", C.c_double), ("lds_bytes_per_block", C.c_int64),
                 ("checkpoint_interval", C.c_int32), ("heading_staging", C.c_int32), ("state_placement", C.c_int32),
-                ("waves_per_simd", C.c_int32)]
+                ("waves_per_simd", C.c_int32), ("constraint_slots", C.c_int32), ("cf_stride", C.c_int32),
+                ("cd_stride", C.c_int32)]
 
 
 class MbikError(RuntimeError):

@@ -1663,6 +1663,9 @@ int32_t mbik_plan_get_info(const mbik_plan *p, mbik_plan_info *o) {
 	o->heading_staging = h.staging ? 1 : 0;
 	o->state_placement = h.state_hbm;
 	o->waves_per_simd = h.waves_per_simd;
+	o->constraint_slots = h.NC;
+	o->cf_stride = h.cf_stride();
+	o->cd_stride = h.cd_stride();
 	return MBIK_OK;
 }
 
@@ -1751,10 +1754,12 @@ int32_t mbik_plan_rebuild_setup(mbik_plan *p, int32_t first, int32_t count, cons
 			static_cast<char *>(scratch), stride, const_cast<float *>(d.D), const_cast<float *>(d.CF),
 			const_cast<double *>(d.CD));
 	hipError_t e = hipGetLastError();
-	// the scratch is freed after the kernel: hipFree synchronizes the device
-	(void)hipStreamSynchronize(st);
+	// the scratch is freed after the kernel; a fault while it runs surfaces at this sync and
+	// must not be reported as success (the D/CF/CD tables may be partly written)
+	hipError_t es = hipStreamSynchronize(st);
 	(void)hipFree(scratch);
 	if (e != hipSuccess) return fail(MBIK_EHIP, std::string("setup launch: ") + hipGetErrorString(e));
+	if (es != hipSuccess) return fail(MBIK_EHIP, std::string("setup kernel: ") + hipGetErrorString(es));
 	// a rebuilt tree starts with fresh node caches (_bone_list_changed)
 	if (h.constraint_mode) return cmode_reset(p, first, count, setup_pose, st);
 	return MBIK_OK;
@@ -1844,6 +1849,13 @@ int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const flo
 		float *pose_out, void *hip_stream) {
 	if (!p) return fail(MBIK_EINVAL, "null plan");
 	if (count <= 0) return MBIK_OK;
+	{
+		// every candidate is timed on the same input: an in-place call would advance the
+		// caller's pose by one frame per timed run
+		const size_t bytes = (size_t)count * p->host.B * 10 * sizeof(float);
+		const char *a = reinterpret_cast<const char *>(pose_in), *b = reinterpret_cast<const char *>(pose_out);
+		if (a && b && a < b + bytes && b < a + bytes) return fail(MBIK_EINVAL, "autotune needs pose_in and pose_out not to overlap");
+	}
 	DeviceGuard guard(p->device);
 	hipStream_t st = reinterpret_cast<hipStream_t>(hip_stream);
 	if (p->host.constraint_mode) return cmode_autotune(p, first, count, pose_in, targets, pose_out, st);

@@ -293,14 +293,16 @@ class ManyBoneIK3D:
 
     # ----------------------------------------------------------------- plan / solve
     def _pin_list(self):
-        out = []
-        for p in self._pins:
-            b = self.find_bone(p["name"])
-            if b < 0:
-                continue
-            out.append(dict(bone=b, weight=p["weight"], direction_priorities=p["direction_priorities"],
-                            motion_propagation_factor=p["motion_propagation_factor"]))
-        return out
+        """Pins whose bone name resolves, in pin order (an unnamed or unknown-bone pin gets no
+        effector, as the reference's segmentation finds no bone for it)."""
+        return [dict(bone=self.find_bone(self._pins[i]["name"]), weight=self._pins[i]["weight"],
+                     direction_priorities=self._pins[i]["direction_priorities"],
+                     motion_propagation_factor=self._pins[i]["motion_propagation_factor"])
+                for i in self._resolved_pin_indices()]
+
+    def _resolved_pin_indices(self) -> list[int]:
+        """Pin indices (into get_pin_count()'s list) that the plan's effectors stand for, in order."""
+        return [i for i, p in enumerate(self._pins) if self.find_bone(p["name"]) >= 0]
 
     def _constraint_arrays(self, n: int):
         cons, cones, twist = [], [], []
@@ -344,12 +346,21 @@ class ManyBoneIK3D:
     def process_modification(self, pose_in, targets, cones=None, twist=None):
         """== ManyBoneIK3D::_process_modification for every skeleton of the batch.
 
-        pose_in [n][bones][10] and targets [n][pins][12] (numpy, host).  The plan is
-        rebuilt from pose_in when dirty, exactly when the reference calls _bone_list_changed.
+        pose_in [n][bones][10] and targets [n][pins][12] (numpy, host), one target row per pin
+        index of get_pin_count()'s list, as each IKEffector3D reads its own target node.  Rows
+        of pins whose bone does not resolve are ignored.  The plan is rebuilt from pose_in when
+        dirty, exactly when the reference calls _bone_list_changed.
         """
         pose_in = np.ascontiguousarray(pose_in, np.float32)
         if self.get_effector_count() == 0 or not self._pins:   # :649-651 and the has_pins check (:669-678)
             return pose_in.copy()
+        targets = np.asarray(targets, np.float32)
+        if targets.ndim != 3 or targets.shape[0] != pose_in.shape[0] or targets.shape[1] != len(self._pins) \
+                or targets.shape[2] != 12:
+            raise ValueError(f"targets must be [n][{len(self._pins)} pins][12], got {targets.shape}")
         if self._dirty or self._plan is None or self._plan.n != pose_in.shape[0]:
             self._bone_list_changed(pose_in, cones, twist)
-        return self._plan.solve_host(pose_in, targets)
+        resolved = self._resolved_pin_indices()
+        if not resolved:                                        # no pin names a bone: nothing to solve
+            return pose_in.copy()
+        return self._plan.solve_host(pose_in, np.ascontiguousarray(targets[:, resolved]))

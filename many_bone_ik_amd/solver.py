@@ -162,7 +162,8 @@ class Plan:
         inf = self.info()
         n, B = inf["skeleton_count"], inf["bone_count"]
         D = np.zeros((B, 9, n), np.float32)
-        slots, cfs, cds = self._slots, self._cf_stride, self._cd_stride
+        slots, cfs, cds = inf["constraint_slots"], inf["cf_stride"], inf["cd_stride"]
+        assert (slots, cfs, cds) == (self._slots, self._cf_stride, self._cd_stride)  # mbik.h's documented formula
         CF = np.zeros((slots, cfs, n), np.float32)
         CD = np.zeros((slots, cds, n), np.float64)
         check(self._L.mbik_plan_setup_tables(self.h, _ptr(D), _ptr(CF) if slots else None, _ptr(CD) if slots else None))

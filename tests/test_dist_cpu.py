@@ -54,3 +54,35 @@ def test_gloo_world2_shard_and_gather(oracle, tmp_path):
     ref = oracle.Oracle(wl).solve(wl.pose, wl.targets)
     got = np.load(out_path)
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+def _bench(*args, env=None):
+    import json
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    e = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    e.update(env or {})
+    r = subprocess.run([sys.executable, os.path.join(here, "bench.py"), *args], capture_output=True, text=True,
+                       timeout=300, env=e, cwd=here)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    return r.returncode, (json.loads(lines[-1]) if lines else None), r.stderr
+
+
+@pytest.mark.parametrize("scaling,total", [("weak", 2 * 7), ("strong", 7)])
+def test_bench_launches_its_own_ranks(scaling, total):
+    """`bench.py --gpus 2` as a plain command (how the driver's scaling run may call it) starts
+    torch.distributed.run itself; the line reports n_gpus == --gpus and the gathered shards
+    cover the batch in order (dry run: gloo, no GPU, no solve)."""
+    rc, line, err = _bench("--gpus", "2", "--dry-run", "--steps", "2", "--warmup", "1", "--skeletons", "7",
+                           "--scaling", scaling)
+    assert rc == 0, err[-2000:]
+    assert line["dry_run"] and line["n_gpus"] == 2 and line["scaling"] == scaling
+    assert line["config"]["skeletons_total"] == total
+    assert line["gathered_in_order"]
+
+
+def test_bench_refuses_world_mismatch():
+    rc, line, err = _bench("--gpus", "4", "--dry-run", env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert rc != 0 and line is None
+    assert "one rank per GPU" in err

@@ -118,6 +118,33 @@ def test_host_api_mirror_end_to_end(oracle, mbik):
     assert_parity(got, ref, "ManyBoneIK3D mirror")
 
 
+def test_mirror_keeps_pin_identity_with_unresolved_pins(oracle, mbik):
+    """An unnamed pin and a pin naming no bone get no effector, but targets stay indexed by pin:
+    each effector reads its own pin's row (an IKEffector3D reads its own target node)."""
+    wl = W.generate(2, 8)
+    ik = ManyBoneIK3D(wl.topo.parents)
+    ik.set_iterations_per_frame(16)
+    ik.set_total_effector_count(6)
+    names = [f"bone_{wl.topo.pins[0]}", "", f"bone_{wl.topo.pins[1]}", "no_such_bone",
+             f"bone_{wl.topo.pins[2]}", f"bone_{wl.topo.pins[3]}"]
+    rows = [0, None, 1, None, 2, 3]
+    for i, nm in enumerate(names):
+        ik.set_effector_bone_name(i, nm)
+        ik.set_pin_weight(i, 1.0)
+    ik._set_constraint_count(len(wl.topo.constrained))
+    for i, b in enumerate(wl.topo.constrained):
+        ik.set_constraint_name_at_index(i, f"bone_{b}")
+        ik.set_kusudama_open_cone_count(i, 2)
+        ik.set_joint_twist(i, (0.0, math.tau))
+    targets = np.full((8, 6, 12), 1e6, np.float32)          # unresolved pins' rows: junk, must be ignored
+    for i, r in enumerate(rows):
+        if r is not None:
+            targets[:, i] = wl.targets[:, r]
+    got = ik.process_modification(wl.pose, targets, cones=wl.cones, twist=wl.twist)
+    ref = oracle.Oracle(wl).solve(wl.pose, wl.targets)
+    assert_parity(got, ref, "mirror with unresolved pins")
+
+
 def test_rig_loaded_from_scene_properties(oracle, mbik):
     """A rig configured from Godot scene properties (many_bone_ik_amd.config), solved on the
     GPU through the ManyBoneIK3D mirror, vs the oracle given the same configuration."""

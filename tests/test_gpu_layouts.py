@@ -78,6 +78,23 @@ def test_autotune_keeps_results(oracle, mbik):
     assert_parity(po.cpu().numpy(), ref, "C2 after autotune")
 
 
+@pytest.mark.parametrize("constraint_mode", [False, True])
+def test_autotune_refuses_overlapping_buffers(mbik, constraint_mode):
+    """Every candidate layout is timed on the same input, so pose_in and pose_out must not
+    overlap (mbik.h); an in-place call would advance the caller's pose once per timed run."""
+    import torch
+    wl = W.generate(3, 64)
+    plan = Plan.from_workload(wl, constraint_mode=constraint_mode)
+    pi = torch.from_numpy(wl.pose).to("cuda:0")
+    tg = torch.from_numpy(wl.targets).to("cuda:0")
+    for out_ptr in (pi.data_ptr(), pi[1:].data_ptr()):
+        with pytest.raises(_lib.MbikError) as e:
+            plan.autotune(pi.data_ptr(), tg.data_ptr(), out_ptr)
+        assert e.value.code == _lib.MBIK_EINVAL
+    before = pi.cpu().numpy()
+    assert np.array_equal(before, wl.pose)
+
+
 @pytest.mark.parametrize("cfg,n", [(2, 48), (3, 48), (4, 16), (5, 6)])
 @pytest.mark.parametrize("stab", [0, 2])
 @pytest.mark.parametrize("lanes", [0, 16])

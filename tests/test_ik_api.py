@@ -3,6 +3,7 @@ src/many_bone_ik_3d.{h,cpp} and src/ik_effector_template_3d.h."""
 import math
 
 import numpy as np
+import pytest
 
 from many_bone_ik_amd.ik import ManyBoneIK3D
 
@@ -125,3 +126,15 @@ def test_register_skeleton_and_editor_state():
     assert ik.get_effector_pin_node_path(0) == ""
     ik.set_effector_pin_node_path(0, "../Target")
     assert ik.get_effector_pin_node_path(0) == "../Target"
+
+
+def test_process_modification_wants_one_target_row_per_pin():
+    """targets are indexed by pin (get_pin_count()), resolved or not; a compacted array is an
+    error before any device work."""
+    ik = ManyBoneIK3D(np.array([-1, 0, 1], np.int32))
+    ik.set_total_effector_count(2)
+    ik.set_effector_bone_name(0, "bone_2")                 # pin 1 stays unnamed
+    pose = np.zeros((3, 3, 10), np.float32)
+    with pytest.raises(ValueError, match="2 pins"):
+        ik.process_modification(pose, np.zeros((3, 1, 12), np.float32))
+    assert ik._resolved_pin_indices() == [0]
