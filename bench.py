@@ -91,7 +91,11 @@ def cpu_baseline(cfg: int, seconds: float, **flags):
     from many_bone_ik_amd import workloads as W
     from oracle import pyoracle as po
     hc = host_cpu()
-    threads = hc["nproc"]
+    # every core this process may use: the affinity set (`nproc`), capped by the cgroup CPU
+    # quota when one is set -- on the GPU box the affinity set is the whole 256-thread machine
+    # but the quota is 16 CPUs, and 256 threads on 16 CPUs only get throttled (31.5 k vs 37.8 k
+    # skeletons/s measured)
+    threads = hc["nproc"] if not hc["cgroup_quota_cpus"] else max(1, min(hc["nproc"], math.ceil(hc["cgroup_quota_cpus"])))
     n = max(512, 8 * threads) if cfg in (2, 3, 4) else max(64, 2 * threads)
     wl = W.generate(cfg, n)
     o = po.Oracle(wl, **flags)
@@ -238,7 +242,7 @@ def main():
             k = min(64, n)
             sub = W.generate(cfg, k, first=first)
             o = po.Oracle(sub, **flags)
-            ref = o.solve(sub.pose, sub.targets, threads=len(os.sched_getaffinity(0)))
+            ref = o.solve(sub.pose, sub.targets, threads=16)
             if args.constraint_mode:  # frames advance the node caches: compare a fresh first frame
                 sp = Plan.from_workload(sub, device=local_rank, **flags)
                 got = sp.solve_host(sub.pose, sub.targets)

@@ -43,6 +43,78 @@ GDI float gd_sqrt(float x) {
 GDI float gd_sqrt(float x) { return sqrtf(x); }
 #endif
 
+// Float quotient a / b, correctly rounded (IEEE), as the reference's x86 divss.
+// On the device: r = 1/(double)b from v_rcp_f64 and one Newton step (relative error ~2^-52),
+// q0 = (double)a * r, one fp64 residual correction q1 = q0 + (a - b*q0) * r, rounded once to
+// float; v_div_fixup_f32 supplies the IEEE result for zero / infinite / NaN operands.  Exact:
+// a quotient of two floats that is not a float rounding midpoint lies at least 2^-49 (relative)
+// from every midpoint, far beyond q1's error; a midpoint quotient (possible only for denormal
+// results) is a double, which the residual correction lands on exactly, so the final rounding
+// ties to even as IEEE does.  tools/div_exact_check.hip checks special pairs, all 2^32
+// dividends for a set of divisors, random pairs and constructed midpoints on the device.
+// A divisor shared by several quotients (normalized(), divs()) computes its reciprocal once.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(MBIK_IEEE_DIV)
+struct GdRcp {
+	float b;
+	double bd, r;
+};
+GDI GdRcp gd_rcp(float b) {
+	const double bd = b;
+	double r = __builtin_amdgcn_rcp(bd);
+	const double e = fma(-bd, r, 1.0);
+	return GdRcp{b, bd, fma(e, r, r)};
+}
+GDI float gd_quot(float a, const GdRcp &d) {
+	const double ad = a;
+	const double q0 = ad * d.r;
+	const double rem = fma(-d.bd, q0, ad);
+	return __builtin_amdgcn_div_fixupf((float)fma(rem, d.r, q0), d.b, a);
+}
+#else
+struct GdRcp {
+	float b;
+};
+GDI GdRcp gd_rcp(float b) { return GdRcp{b}; }
+GDI float gd_quot(float a, const GdRcp &d) { return a / d.b; }
+#endif
+GDI float gd_div(float a, float b) { return gd_quot(a, gd_rcp(b)); }
+// N / b for a power-of-two constant N (0.5f, 1.0f, 2.0f: Basis::set_quaternion's 2/d,
+// get_quaternion's 0.5/s, inverse's 1/det, ...).  (double)N * r is r scaled exactly, so the
+// quotient is one rounding of r, and no residual correction is needed: such a quotient is
+// never a float rounding midpoint (N/b = m * 2^-150 with m odd would need b = N * 2^150 / m,
+// not a float), and r is far closer to N/b than any midpoint.  tools/div_exact_check.hip
+// checks all 2^32 divisors for N = 0.5, 1, 2.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(MBIK_IEEE_DIV)
+GDI float gd_pow2_over(float n, float b) {
+	const GdRcp d = gd_rcp(b);
+	return __builtin_amdgcn_div_fixupf((float)((double)n * d.r), b, n);
+}
+#else
+GDI float gd_pow2_over(float n, float b) { return n / b; }
+#endif
+
+// x / RN(sqrt(l)) for several x at once (normalized()): the square root as gd_sqrt, and the
+// reciprocal of the rounded root refined from the same v_rsq_f64 estimate (one Newton step,
+// ~2^-44) instead of a separate v_rcp_f64; the quotients as gd_quot.  Same exactness argument
+// (the residual correction squares the reciprocal's error).  Host: sqrtf and IEEE division.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(MBIK_IEEE_DIV) && !defined(MBIK_IEEE_SQRT)
+GDI GdRcp gd_sqrt_rcp(float l, float &len) {
+	const double ld = l;
+	const double y = __builtin_amdgcn_rsq(ld);
+	const double g = ld * y, h = 0.5 * y;
+	const double e = fma(-g, g, ld);
+	len = __builtin_amdgcn_class(l, 0x260) ? l : (float)fma(e, h, g);
+	const double Ld = len;
+	const double e2 = fma(-Ld, y, 1.0);
+	return GdRcp{len, Ld, fma(e2, y, y)};
+}
+#else
+GDI GdRcp gd_sqrt_rcp(float l, float &len) {
+	len = gd_sqrt(l);
+	return gd_rcp(len);
+}
+#endif
+
 // ---------------- Float transcendentals: the platform libm of the reference ----------------
 // Godot's Math::sin/cos/acos(float) call ::sinf/::cosf/::acosf (core/math/math_funcs.h).  On
 // the reference's Linux x86-64 build that is glibc; the solve amplifies a 1-ulp libm
@@ -201,6 +273,10 @@ GDI float slerp_scale0(float omega) {
 	return (float)(sin((double)omega) / (double)sinom);
 }
 
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(MBIK_NO_PACK)
+#define GD_PACK 1
+typedef float F2 __attribute__((ext_vector_type(2)));
+#endif
 struct V3 {
 	float x, y, z;
 	GDI float operator[](int i) const { return i == 0 ? x : (i == 1 ? y : z); }
@@ -217,32 +293,55 @@ struct X3 { // Transform3D
 };
 
 GDI V3 v3(float x, float y, float z) { return V3{x, y, z}; }
-GDI V3 operator+(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+// Packed-pair arithmetic (device): the x and y lanes of a vector op go through one
+// v_pk_{add,mul}_f32 (two IEEE float operations, each rounded exactly as the scalar one),
+// z through a scalar op; sums keep the reference's left-to-right order.  One wave issues a
+// packed op in about the time of a scalar one (tools/ubench.hip), so this is up to a third
+// fewer VALU cycles for vector and basis arithmetic.
+#ifdef GD_PACK
+GDI F2 f2(float a, float b) { return F2{a, b}; }
+GDI F2 xy(V3 a) { return F2{a.x, a.y}; }
+GDI V3 v3(F2 p, float z) { return V3{p.x, p.y, z}; }
+#endif
+// (subtraction stays scalar: packing it made the compiler keep V3 temporaries on the stack)
 GDI V3 operator-(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
-GDI V3 operator-(V3 a) { return v3(-a.x, -a.y, -a.z); }
+#ifdef GD_PACK
+GDI V3 operator+(V3 a, V3 b) { return v3(xy(a) + xy(b), a.z + b.z); }
+GDI V3 operator*(V3 a, float s) { return v3(xy(a) * s, a.z * s); }
+GDI V3 mulv(V3 a, V3 b) { return v3(xy(a) * xy(b), a.z * b.z); }
+GDI float dot(V3 a, V3 b) {
+	const F2 p = xy(a) * xy(b);
+	return (p.x + p.y) + a.z * b.z;
+}
+GDI float length_sq(V3 a) {
+	const F2 p = xy(a) * xy(a);
+	return (p.x + p.y) + a.z * a.z;
+}
+#else
+GDI V3 operator+(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
 GDI V3 operator*(V3 a, float s) { return v3(a.x * s, a.y * s, a.z * s); }
 GDI V3 mulv(V3 a, V3 b) { return v3(a.x * b.x, a.y * b.y, a.z * b.z); }
-GDI V3 divs(V3 a, float s) { return v3(a.x / s, a.y / s, a.z / s); }
 GDI float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
-GDI V3 cross(V3 a, V3 b) { return v3((a.y * b.z) - (a.z * b.y), (a.z * b.x) - (a.x * b.z), (a.x * b.y) - (a.y * b.x)); }
 GDI float length_sq(V3 a) {
 	float x2 = a.x * a.x, y2 = a.y * a.y, z2 = a.z * a.z;
 	return x2 + y2 + z2;
 }
+#endif
+GDI V3 operator-(V3 a) { return v3(-a.x, -a.y, -a.z); }
+GDI V3 divs(V3 a, float s) {
+	const GdRcp d = gd_rcp(s);
+	return v3(gd_quot(a.x, d), gd_quot(a.y, d), gd_quot(a.z, d));
+}
+GDI V3 cross(V3 a, V3 b) { return v3((a.y * b.z) - (a.z * b.y), (a.z * b.x) - (a.x * b.z), (a.x * b.y) - (a.y * b.x)); }
 GDI float length(V3 a) { return gd_sqrt(length_sq(a)); }
 GDI V3 normalized(V3 a) {
 	float l = length_sq(a);
 	if (l == 0) return v3(0, 0, 0);
-	float len = gd_sqrt(l);
-#ifdef MBIK_ABLATE_NORMDIV
-	float r = 1.0f / len; // timing experiment only
-	return v3(a.x * r, a.y * r, a.z * r);
-#else
-	// IEEE quotients.  A shared fp64 reciprocal ((float)((double)a * r), exact except for
-	// denormal quotients -- tools/div_check.hip) measured slower in the kernel once the
-	// denormal/range guard branch is paid (C2 1.596 vs 1.525 ms).
-	return v3(a.x / len, a.y / len, a.z / len);
-#endif
+	// IEEE quotients by the rounded length (gd_sqrt_rcp / gd_quot: one reciprocal shared by
+	// the three components)
+	float len;
+	const GdRcp d = gd_sqrt_rcp(l, len);
+	return v3(gd_quot(a.x, d), gd_quot(a.y, d), gd_quot(a.z, d));
 }
 GDI bool is_zero_approx(float s) { return fabsf(s) < (float)CMP_EPSILON; }
 GDI bool is_equal_approx(float a, float b) {
@@ -263,9 +362,24 @@ GDI V3 any_perpendicular(V3 a) {
 // ---------------- Quaternion ----------------
 GDI Q q4(float x, float y, float z, float w) { return Q{x, y, z, w}; }
 GDI Q qid() { return Q{0, 0, 0, 1}; }
+#ifdef GD_PACK
+GDI float dot(Q a, Q b) {
+	const F2 p = f2(a.x, a.y) * f2(b.x, b.y), q = f2(a.z, a.w) * f2(b.z, b.w);
+	return ((p.x + p.y) + q.x) + q.y;
+}
+GDI Q operator*(Q a, float s) {
+	const F2 p = f2(a.x, a.y) * s, q = f2(a.z, a.w) * s;
+	return q4(p.x, p.y, q.x, q.y);
+}
+#else
 GDI float dot(Q a, Q b) { return a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w; }
 GDI Q operator*(Q a, float s) { return q4(a.x * s, a.y * s, a.z * s, a.w * s); }
-GDI Q normalized(Q a) { return a * (1.0f / gd_sqrt(dot(a, a))); } // operator/ multiplies by 1/s
+#endif
+GDI Q normalized(Q a) { // operator/ multiplies by 1/s
+	float len;
+	const GdRcp d = gd_sqrt_rcp(dot(a, a), len);
+	return a * gd_quot(1.0f, d);
+}
 GDI Q inverse(Q a) { return q4(-a.x, -a.y, -a.z, a.w); }
 GDI Q operator*(Q a, Q b) {
 	float xx = a.w * b.x + a.x * b.w + a.y * b.z - a.z * b.y;
@@ -321,12 +435,12 @@ GDI Q arc(V3 v0, V3 v1) {
 	}
 	V3 c = cross(n0, n1);
 	float s = gd_sqrt((1.0f + d) * 2.0f);
-	float rs = 1.0f / s;
+	float rs = gd_pow2_over(1.0f, s);
 	return q4(c.x * rs, c.y * rs, c.z * rs, s * 0.5f);
 }
 GDI V3 get_axis(Q q) {
 	if (fabsf(q.w) > 1 - CMP_EPSILON) return v3(q.x, q.y, q.z);
-	float r = 1.0f / gd_sqrt(1 - q.w * q.w);
+	float r = gd_pow2_over(1.0f, gd_sqrt(1 - q.w * q.w));
 	return v3(q.x * r, q.y * r, q.z * r);
 }
 GDI float get_angle(Q q) { return 2 * acos_f(q.w); }
@@ -346,7 +460,7 @@ GDI B3 from_cols(V3 x, V3 y, V3 z) { return bset(x.x, y.x, z.x, x.y, y.y, z.y, x
 // Basis::set_quaternion
 GDI B3 from_quat(Q q) {
 	float d = dot(q, q);
-	float s = 2.0f / d;
+	float s = gd_pow2_over(2.0f, d);
 	float xs = q.x * s, ys = q.y * s, zs = q.z * s;
 	float wx = q.w * xs, wy = q.w * ys, wz = q.w * zs;
 	float xx = q.x * xs, xy = q.x * ys, xz = q.x * zs;
@@ -361,24 +475,24 @@ GDI Q get_quaternion(const B3 &m) {
 	if (trace > 0.0f) {
 		float s = gd_sqrt(trace + 1.0f);
 		float w = s * 0.5f;
-		s = 0.5f / s;
+		s = gd_pow2_over(0.5f, s);
 		return q4((m.r[2].y - m.r[1].z) * s, (m.r[0].z - m.r[2].x) * s, (m.r[1].x - m.r[0].y) * s, w);
 	}
 	int i = r00 < r11 ? (r11 < r22 ? 2 : 1) : (r00 < r22 ? 2 : 0);
 	if (i == 0) { // j = 1, k = 2
 		float s = gd_sqrt(r00 - r11 - r22 + 1.0f);
 		float ti = s * 0.5f;
-		s = 0.5f / s;
+		s = gd_pow2_over(0.5f, s);
 		return q4(ti, (m.r[1].x + m.r[0].y) * s, (m.r[2].x + m.r[0].z) * s, (m.r[2].y - m.r[1].z) * s);
 	} else if (i == 1) { // j = 2, k = 0
 		float s = gd_sqrt(r11 - r22 - r00 + 1.0f);
 		float ti = s * 0.5f;
-		s = 0.5f / s;
+		s = gd_pow2_over(0.5f, s);
 		return q4((m.r[0].y + m.r[1].x) * s, ti, (m.r[2].y + m.r[1].z) * s, (m.r[0].z - m.r[2].x) * s);
 	} else { // i = 2: j = 0, k = 1
 		float s = gd_sqrt(r22 - r00 - r11 + 1.0f);
 		float ti = s * 0.5f;
-		s = 0.5f / s;
+		s = gd_pow2_over(0.5f, s);
 		return q4((m.r[0].z + m.r[2].x) * s, (m.r[1].z + m.r[2].y) * s, ti, (m.r[1].x - m.r[0].y) * s);
 	}
 }
@@ -411,7 +525,7 @@ GDI Q get_rotation_quaternion(const B3 &b) {
 GDI B3 inverse(const B3 &b) {
 	float co0 = GD_COF(b, 1, 1, 2, 2), co1 = GD_COF(b, 1, 2, 2, 0), co2 = GD_COF(b, 1, 0, 2, 1);
 	float det = b.r[0].x * co0 + b.r[0].y * co1 + b.r[0].z * co2;
-	float s = 1.0f / det;
+	float s = gd_pow2_over(1.0f, det);
 	return bset(co0 * s, GD_COF(b, 0, 2, 2, 1) * s, GD_COF(b, 0, 1, 1, 2) * s, co1 * s, GD_COF(b, 0, 0, 2, 2) * s,
 			GD_COF(b, 0, 2, 1, 0) * s, co2 * s, GD_COF(b, 0, 1, 2, 0) * s, GD_COF(b, 0, 0, 1, 1) * s);
 }
@@ -426,8 +540,12 @@ GDI B3 operator*(const B3 &a, const B3 &b) {
 #pragma unroll
 	for (int i = 0; i < 3; i++) {
 		V3 ar = a.r[i];
+#ifdef GD_PACK
+		r.r[i] = v3((xy(b.r[0]) * ar.x + xy(b.r[1]) * ar.y) + xy(b.r[2]) * ar.z, b.r[0].z * ar.x + b.r[1].z * ar.y + b.r[2].z * ar.z);
+#else
 		r.r[i] = v3(b.r[0].x * ar.x + b.r[1].x * ar.y + b.r[2].x * ar.z, b.r[0].y * ar.x + b.r[1].y * ar.y + b.r[2].y * ar.z,
 				b.r[0].z * ar.x + b.r[1].z * ar.y + b.r[2].z * ar.z);
+#endif
 	}
 	return r;
 }
