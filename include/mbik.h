@@ -249,6 +249,24 @@ int32_t mbik_describe_topology(const mbik_skeleton_desc *desc, const mbik_config
  * exactly one of them is NaN.  Both must be 0 (gd_math.h: gd_sqrt). */
 int32_t mbik_selftest_math(int32_t device, uint64_t out[2]);
 
+/* Device self-test of the kernel's float quotients (gd_math.h: an fp64 reciprocal with a
+ * residual correction, or one rounding for power-of-two numerators) against IEEE division:
+ * out[c] = mismatching results of class c below (two NaNs compare equal), out[8 + 2c] and
+ * out[9 + 2c] the operand bit patterns of one mismatch.  All counts must be 0.
+ *   SPECIALS          every pair of 24 special values (zeros, infinities, NaNs, denormals, extremes)
+ *   ALL_DIVIDENDS     all 2^32 dividends for 12 divisors
+ *   RANDOM            random_iterations x 2^21 random pairs (free and close exponents)
+ *   MIDPOINTS         random_iterations x 2^21 constructed denormal midpoint quotients
+ *   POW2_NUMERATOR    0.5 / b, 1 / b, 2 / b for all 2^32 divisors
+ *   NORMALIZE         a / sqrtf(l) (normalized()) and the root itself for all 2^32 l, 8 values of a */
+#define MBIK_DIV_SPECIALS 0
+#define MBIK_DIV_ALL_DIVIDENDS 1
+#define MBIK_DIV_RANDOM 2
+#define MBIK_DIV_MIDPOINTS 3
+#define MBIK_DIV_POW2_NUMERATOR 4
+#define MBIK_DIV_NORMALIZE 5
+int32_t mbik_selftest_div(int32_t device, uint64_t random_iterations, uint64_t out[20]);
+
 /* Device self-test of the solve's transcendental call sites against values the caller
  * computed with the host's libm (the reference's: Godot's Math::sin/cos/acos call ::sinf,
  * ::cosf, ::acosf and ::sin/::cos; glibc on Linux x86-64).  For fn = SINF, COSF, ACOSF,

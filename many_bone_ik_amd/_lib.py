@@ -27,7 +27,7 @@ EXPORTED_SYMBOLS = (
     "mbik_plan_set_locals_placement", "mbik_plan_set_waves_per_simd", "mbik_plan_rebuild_setup", "mbik_plan_setup_tables",
     "mbik_solve", "mbik_solve_checked", "mbik_solve_host", "mbik_segment_solve", "mbik_plan_segment_table", "mbik_describe_topology",
     "mbik_group_create", "mbik_group_solve", "mbik_group_destroy", "mbik_capture_targets", "mbik_selftest_math",
-    "mbik_selftest_libm", "mbik_last_error",
+    "mbik_selftest_libm", "mbik_selftest_div", "mbik_last_error",
 )
 
 
@@ -122,6 +122,8 @@ def load():
     L.mbik_solve_checked.restype = C.c_int32
     L.mbik_selftest_math.argtypes = [C.c_int32, C.POINTER(C.c_uint64)]
     L.mbik_selftest_math.restype = C.c_int32
+    L.mbik_selftest_div.argtypes = [C.c_int32, C.c_uint64, C.POINTER(C.c_uint64)]
+    L.mbik_selftest_div.restype = C.c_int32
     L.mbik_selftest_libm.argtypes = [C.c_int32, C.c_uint64, C.c_uint64, vp, vp, C.POINTER(C.c_uint64), vp]
     L.mbik_selftest_libm.restype = C.c_int32
     L.mbik_solve_host.argtypes = [vp, C.c_int32, C.c_int32, vp, vp, vp]

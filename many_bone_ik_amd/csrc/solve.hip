@@ -1989,6 +1989,91 @@ __global__ void mbik_selftest_math_kernel(unsigned long long *out) {
 	if (bad) atomicAdd(&out[0], bad);
 	if (nan_bad) atomicAdd(&out[1], nan_bad);
 }
+// mbik_selftest_div: the kernel's float quotients (gd_math.h gd_quot / gd_pow2_over /
+// gd_sqrt_rcp) against the compiler's IEEE division.  out[c] counts mismatches per class c
+// (MBIK_DIV_*); out[8 + 2c], out[9 + 2c] keep the bit patterns of one mismatching operand pair.
+__device__ __forceinline__ uint64_t st_mix(uint64_t &s) {
+	uint64_t z = (s += 0x9e3779b97f4a7c15ull);
+	z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+	z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+	return z ^ (z >> 31);
+}
+__device__ __forceinline__ bool same_f(float x, float y) { return __float_as_uint(x) == __float_as_uint(y) || (x != x && y != y); }
+__device__ __forceinline__ void div_tally(unsigned long long *out, int cls, float ref, float got, float a, float b) {
+	if (same_f(ref, got)) return;
+	if (atomicAdd(&out[cls], 1ull) == 0ull) {
+		out[8 + 2 * cls] = __float_as_uint(a);
+		out[9 + 2 * cls] = __float_as_uint(b);
+	}
+}
+__device__ const unsigned kDivSpecials[] = {0x00000000u, 0x80000000u, 0x7f800000u, 0xff800000u, 0x7fc00000u, 0xffc00001u,
+		0x00000001u, 0x80000003u, 0x007fffffu, 0x807fffffu, 0x00800000u, 0x7f7fffffu, 0xff7fffffu, 0x3f800000u, 0xbf800000u,
+		0x3f7fffffu, 0x3f800001u, 0x34000000u, 0x5f000000u, 0x1f800000u, 0x00400000u, 0x7f000000u, 0x40400000u, 0x3dcccccdu};
+__device__ const unsigned kDivFixed[] = {0x3f800000u, 0x40000000u, 0x3f800001u, 0x3f7fffffu, 0x40400000u, 0x3dcccccdu,
+		0x4049a0b1u, 0x00000003u, 0x00400001u, 0x7e800001u, 0xbf9d70a4u, 0x3a83126fu};
+// dividends of normalized(): a component against the rounded length of its vector
+__device__ const unsigned kDivNormA[] = {0x3f800000u, 0x3f333333u, 0x0da24260u, 0x00200000u, 0xc0200000u, 0x00000001u,
+		0x7f7fffffu, 0x80000000u};
+__global__ void mbik_selftest_div_kernel(int cls, int sel, uint64_t iters, unsigned long long *out) {
+	const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, nthreads = (uint64_t)gridDim.x * blockDim.x;
+	constexpr int NS = sizeof(kDivSpecials) / sizeof(kDivSpecials[0]);
+	if (cls == MBIK_DIV_SPECIALS) {
+		if (tid < NS * NS) {
+			const float a = __uint_as_float(kDivSpecials[tid % NS]), b = __uint_as_float(kDivSpecials[tid / NS]);
+			div_tally(out, cls, a / b, gd_div(a, b), a, b);
+		}
+	} else if (cls == MBIK_DIV_ALL_DIVIDENDS) { // every float dividend, divisor kDivFixed[sel]
+		const float b = __uint_as_float(kDivFixed[sel]);
+		for (uint64_t i = tid; i < (1ull << 32); i += nthreads) {
+			const float a = __uint_as_float((unsigned)i);
+			div_tally(out, cls, a / b, gd_div(a, b), a, b);
+		}
+	} else if (cls == MBIK_DIV_RANDOM) { // random pairs: free exponents, and close exponents
+		uint64_t s = tid * 0x2545f4914f6cdd1dull + 777;
+		for (uint64_t it = 0; it < iters; it++) {
+			const uint64_t z = st_mix(s);
+			unsigned ab = (unsigned)z, bb = (unsigned)(z >> 32);
+			if (it & 1) {
+				ab = (ab & 0x807fffffu) | ((110u + ((z >> 8) & 31)) << 23);
+				bb = (bb & 0x807fffffu) | ((110u + ((z >> 40) & 31)) << 23);
+			}
+			const float a = __uint_as_float(ab), b = __uint_as_float(bb);
+			div_tally(out, cls, a / b, gd_div(a, b), a, b);
+		}
+	} else if (cls == MBIK_DIV_MIDPOINTS) { // exact denormal midpoints m * 2^-150, m odd
+		uint64_t s = tid * 0x9e3779b97f4a7c15ull + 99;
+		for (uint64_t it = 0; it < iters; it++) {
+			const uint64_t z = st_mix(s);
+			const int mbits = 1 + (int)(z % 23);
+			const uint32_t m = ((uint32_t)(z >> 8) & ((1u << mbits) - 1u)) | 1u;
+			const int bbits = 1 + (int)((z >> 40) % (uint64_t)(24 - mbits + 1));
+			const uint32_t B = ((uint32_t)(z >> 20) & ((1u << bbits) - 1u)) | 1u | (1u << (bbits - 1));
+			const int e = 100 + (int)((z >> 50) % 60);
+			const double bd = ldexp((double)B, e - bbits), ad = ldexp((double)((uint64_t)m * B), e - bbits - 150);
+			float a = (float)ad, b = (float)bd;
+			if ((double)a != ad || (double)b != bd) continue;
+			a = (z >> 62) & 1 ? -a : a;
+			b = (z >> 63) ? -b : b;
+			div_tally(out, cls, a / b, gd_div(a, b), a, b);
+		}
+	} else if (cls == MBIK_DIV_POW2_NUMERATOR) { // N / b, N = 0.5, 1, 2, every float b
+		for (uint64_t i = tid; i < (1ull << 32); i += nthreads) {
+			const float b = __uint_as_float((unsigned)i);
+			div_tally(out, cls, 0.5f / b, gd_pow2_over(0.5f, b), 0.5f, b);
+			div_tally(out, cls, 1.0f / b, gd_pow2_over(1.0f, b), 1.0f, b);
+			div_tally(out, cls, 2.0f / b, gd_pow2_over(2.0f, b), 2.0f, b);
+		}
+	} else if (cls == MBIK_DIV_NORMALIZE) { // a / sqrtf(l), every float l, a = kDivNormA[sel]
+		const float a = __uint_as_float(kDivNormA[sel]);
+		for (uint64_t i = tid; i < (1ull << 32); i += nthreads) {
+			const float l = __uint_as_float((unsigned)i);
+			float len;
+			const GdRcp d = gd_sqrt_rcp(l, len);
+			div_tally(out, cls, a / sqrtf(l), gd_quot(a, d), a, l);
+			div_tally(out, cls, sqrtf(l), len, a, l);
+		}
+	}
+}
 // mbik_selftest_libm: the device's transcendental call sites against host-computed values.
 // out[0] = observable mismatches, out[1] = lowest such index (atomicMin; ~0 if none),
 // out[2] = results whose bits differ at all.
@@ -2060,6 +2145,35 @@ int32_t mbik_selftest_math(int32_t device, uint64_t out[2]) {
 	(void)hipFree(d);
 	out[0] = h[0];
 	out[1] = h[1];
+	return rc;
+}
+
+int32_t mbik_selftest_div(int32_t device, uint64_t random_iterations, uint64_t out[20]) {
+	if (!out) return fail(MBIK_EINVAL, "null output");
+	int ndev = 0;
+	if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(MBIK_ENODEV, "no HIP device");
+	if (device < 0 || device >= ndev) return fail(MBIK_EINVAL, "device out of range");
+	DeviceGuard guard(device);
+	unsigned long long *d = nullptr;
+	if (hipMalloc(&d, 20 * sizeof(unsigned long long)) != hipSuccess) return fail(MBIK_ENOMEM, "hipMalloc");
+	int rc = MBIK_OK;
+	if (hipMemset(d, 0, 20 * sizeof(unsigned long long)) != hipSuccess) rc = fail(MBIK_EHIP, "hipMemset");
+	auto run = [&](int cls, int sel) {
+		if (rc != MBIK_OK) return;
+		hipLaunchKernelGGL(mbik_selftest_div_kernel, dim3(8192), dim3(256), 0, 0, cls, sel, random_iterations, d);
+		if (hipGetLastError() != hipSuccess) rc = fail(MBIK_EHIP, "self-test kernel launch");
+	};
+	run(MBIK_DIV_SPECIALS, 0);
+	for (int k = 0; k < 12; k++) run(MBIK_DIV_ALL_DIVIDENDS, k);
+	run(MBIK_DIV_RANDOM, 0);
+	run(MBIK_DIV_MIDPOINTS, 0);
+	run(MBIK_DIV_POW2_NUMERATOR, 0);
+	for (int k = 0; k < 8; k++) run(MBIK_DIV_NORMALIZE, k);
+	if (rc == MBIK_OK && hipDeviceSynchronize() != hipSuccess) rc = fail(MBIK_EHIP, "self-test kernel");
+	unsigned long long h[20] = {};
+	if (rc == MBIK_OK && hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost) != hipSuccess) rc = fail(MBIK_EHIP, "hipMemcpy");
+	(void)hipFree(d);
+	for (int i = 0; i < 20; i++) out[i] = h[i];
 	return rc;
 }
 
