@@ -268,10 +268,46 @@ GDI float acos_f(float x) { return glibc::acosf(x); }
 // denominator sinom = Math::sin(omega) a float sinf.  (scale1 = sinf(0 * omega) / sinom = +0.)
 // The double sin is the device's own (OCML); mbik_selftest_libm proves this quotient equal
 // to the host glibc's for every float omega.
+//
+// Device fast path: sin(omega) by its odd Taylor polynomial through x^21 for |omega| <= 1.6
+// (the solve's omega, an acos of a non-negative cosine, lies in [0, pi/2]; truncation
+// < 2^-58, evaluation < 2^-50 relative), the quotient through an fp64 reciprocal, and the
+// float rounding of the ends of a 2^-46 (relative) interval around that estimate: the exact
+// RN(RN(sin(w) / sinom)) lies inside it (the estimate is within ~2^-48), so when both ends
+// round to the same float, that float is the result.  Otherwise -- essentially never -- the
+// device's own double sin and division run.  mbik_selftest_libm's SLERP_SCALE0 class compares
+// the result with the host glibc's for all 2^32 omega.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(MBIK_EXACT_SLERP_SIN)
+GDI double sin_taylor(double x) {
+	const double x2 = x * x;
+	double p = 0x1.71b8ef6dcf572p-66;        //  1/21!
+	p = fma(p, x2, -0x1.2f49b46814157p-57);  // -1/19!
+	p = fma(p, x2, 0x1.952c77030ad4ap-49);   //  1/17!
+	p = fma(p, x2, -0x1.ae7f3e733b81fp-41);  // -1/15!
+	p = fma(p, x2, 0x1.6124613a86d09p-33);   //  1/13!
+	p = fma(p, x2, -0x1.ae64567f544e4p-26);  // -1/11!
+	p = fma(p, x2, 0x1.71de3a556c734p-19);   //  1/9!
+	p = fma(p, x2, -0x1.a01a01a01a01ap-13);  // -1/7!
+	p = fma(p, x2, 0x1.1111111111111p-7);    //  1/5!
+	p = fma(p, x2, -0x1.5555555555555p-3);   // -1/3!
+	return fma(x * x2, p, x);
+}
+GDI float slerp_scale0(float omega) {
+	const float sinom = sin_f(omega);
+	if (fabsf(omega) <= 1.6f) {
+		const double q = sin_taylor((double)omega) * gd_rcp(sinom).r;
+		const double w = fabs(q) * 0x1p-46;
+		const float lo = (float)(q - w), hi = (float)(q + w);
+		if (lo == hi) return lo; // (a NaN estimate, sinom == 0, falls through)
+	}
+	return (float)(sin((double)omega) / (double)sinom);
+}
+#else
 GDI float slerp_scale0(float omega) {
 	const float sinom = sin_f(omega);
 	return (float)(sin((double)omega) / (double)sinom);
 }
+#endif
 
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(MBIK_NO_PACK)
 #define GD_PACK 1
