@@ -119,6 +119,16 @@ typedef struct mbik_plan_info {
 int32_t mbik_plan_create(const mbik_skeleton_desc *desc, const mbik_config *config, int32_t n_skeletons,
 		const float *setup_pose, const float *cones, const float *twist, int32_t device, mbik_plan **out_plan);
 void mbik_plan_destroy(mbik_plan *plan);
+/* Plan serialisation to a flat binary (checkpoint / resume, or a plan built once and shipped):
+ * the creation inputs (topology, pins, constraints, config), the per-skeleton setup tables as
+ * they are on the device (including any mbik_plan_rebuild_setup), the layout overrides and
+ * autotune choice, and for constraint_mode the persistent node caches.  mbik_plan_save with
+ * buf == NULL stores the needed size in *size; otherwise capacity must be at least that
+ * (MBIK_EINVAL).  It reads the device tables back, so the streams using the plan must be
+ * idle.  mbik_plan_load rebuilds the plan on `device` from such a buffer; the loaded plan
+ * solves bitwise like the saved one.  Format version 1, little-endian, host-independent. */
+int32_t mbik_plan_save(const mbik_plan *plan, void *buf, uint64_t capacity, uint64_t *size);
+int32_t mbik_plan_load(const void *buf, uint64_t size, int32_t device, mbik_plan **out_plan);
 int32_t mbik_plan_get_info(const mbik_plan *plan, mbik_plan_info *out);
 /* Launch-shape override (0 = automatic).  lanes_per_skeleton must be a power of two <= 64. */
 int32_t mbik_plan_set_launch(mbik_plan *plan, int32_t lanes_per_skeleton);

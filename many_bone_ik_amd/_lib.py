@@ -22,7 +22,7 @@ MBIK_ENODEV = -5
 LIBM_SINF, LIBM_COSF, LIBM_ACOSF, LIBM_SLERP_SCALE0, LIBM_COS_F64_OF_F32, LIBM_COS_F64 = range(6)
 
 EXPORTED_SYMBOLS = (
-    "mbik_plan_create", "mbik_plan_destroy", "mbik_plan_get_info", "mbik_plan_set_launch", "mbik_plan_set_layout",
+    "mbik_plan_create", "mbik_plan_destroy", "mbik_plan_save", "mbik_plan_load", "mbik_plan_get_info", "mbik_plan_set_launch", "mbik_plan_set_layout",
     "mbik_plan_autotune", "mbik_plan_resident_blocks", "mbik_plan_set_heading_staging",
     "mbik_plan_set_locals_placement", "mbik_plan_set_waves_per_simd", "mbik_plan_rebuild_setup", "mbik_plan_setup_tables",
     "mbik_solve", "mbik_solve_checked", "mbik_solve_host", "mbik_segment_solve", "mbik_plan_segment_table", "mbik_describe_topology",
@@ -96,6 +96,10 @@ def load():
     L.mbik_plan_create.restype = C.c_int32
     L.mbik_plan_destroy.argtypes = [vp]
     L.mbik_plan_destroy.restype = None
+    L.mbik_plan_save.argtypes = [vp, vp, C.c_uint64, C.POINTER(C.c_uint64)]
+    L.mbik_plan_save.restype = C.c_int32
+    L.mbik_plan_load.argtypes = [vp, C.c_uint64, C.c_int32, C.POINTER(vp)]
+    L.mbik_plan_load.restype = C.c_int32
     L.mbik_plan_get_info.argtypes = [vp, C.POINTER(MbikPlanInfo)]
     L.mbik_plan_get_info.restype = C.c_int32
     L.mbik_plan_set_launch.argtypes = [vp, C.c_int32]

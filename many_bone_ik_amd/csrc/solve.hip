@@ -334,6 +334,7 @@ __device__ __forceinline__ void effector_headings(const DevPlan &t, const EffPre
 		const int off = p.off;
 		const int de = p.de;
 		int d = t.bone_depth[b] + 1;
+#ifndef MBIK_PATH_UNROLL2
 		if (d <= de) {
 			// software-pipelined: the next path bone's local pose loads during this product
 			X3 Ln = L.ld(t.eff_path[off + d]);
@@ -344,6 +345,22 @@ __device__ __forceinline__ void effector_headings(const DevPlan &t, const EffPre
 			}
 			X = X * Ln;
 		}
+#else
+		if (d <= de) {
+			// software-pipelined: the next path bone's local pose loads during this product.
+			// Two load buffers alternate (unrolled by two), so no loop-carried register copy
+			// of the pending transform is needed.
+			X3 La = L.ld(t.eff_path[off + d]), Lb;
+			for (;;) {
+				if (d < de) Lb = L.ld(t.eff_path[off + d + 1]);
+				X = X * La;
+				if (++d > de) break;
+				if (d < de) La = L.ld(t.eff_path[off + d + 1]);
+				X = X * Lb;
+				if (++d > de) break;
+			}
+		}
+#endif
 		E.b = X.b * p.Db;
 		E.o = X.o;
 	}
@@ -870,6 +887,10 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 	const int flags = t.bone_flags[b];
 	bool swung = false;
 	X3 Gbd_stale;
+#ifdef MBIK_GS_REUSE
+	B3 GsB = {};     // P.basis * Lb.basis after the swing check, reused by the twist if not swung
+	bool gs_ok = false;
+#endif
 #ifdef MBIK_ABLATE_SWING
 	if (false) {
 #else
@@ -877,6 +898,10 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 #endif
 		const int slot = t.bone_cons[b];
 		X3 Gs = P * Lb;
+#ifdef MBIK_GS_REUSE
+		GsB = Gs.b;
+		gs_ok = true;
+#endif
 		Gbd_stale.b = Gs.b * ld_soa_basis(t.D, b, 9, 0, t.N, s);
 		Gbd_stale.o = Gs.o;
 		X3 Gco = {P.b, xform(P, Lb.o)}; // constraint_orientation: (I, pose local origin) under the parent
@@ -907,7 +932,13 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 		float half_cos = soa(t.CF, slot, cs, mbik::CF_TWIST_COS, t.N, s);
 		B3 Tb = ld_soa_basis(t.CF, slot, cs, mbik::CF_TWIST_T, t.N, s);
 		B3 Gct = P.b * Tb;
+#ifdef MBIK_GS_REUSE
+		X3 Gs;
+		if (gs_ok && !swung) Gs.b = GsB;
+		else Gs.b = P.b * Lb.b;
+#else
 		X3 Gs = P * Lb;
+#endif
 		B3 gtc = Gct * from_quat(tcr);
 		B3 align = orthonormalized(inverse(gtc) * Gs.b);
 		Q sw, tw;
@@ -1269,6 +1300,13 @@ struct mbik_plan {
 	// constraint_mode: the persistent IKNode3D caches (cmode.h), lanes per skeleton (0 = auto)
 	CmodeState cm{};
 	int cm_lanes = 0;
+	// the creation inputs, for mbik_plan_save (the topology is rebuilt from them on load)
+	std::vector<int32_t> src_parents;
+	std::vector<mbik_pin> src_pins;
+	std::vector<mbik_constraint> src_cons;
+	std::vector<float> src_bone_damp;
+	int32_t src_max_cones = 1;
+	mbik_config src_cfg{};
 };
 
 namespace {
@@ -1448,7 +1486,7 @@ int cmode_reset(mbik_plan *p, int first, int count, const float *setup_pose, hip
 
 // constraint_mode: allocates the persistent node caches and builds the fresh tree from the
 // host setup poses of mbik_plan_create.
-int cmode_create(mbik_plan *p, const float *setup_pose) {
+int cmode_create(mbik_plan *p, const float *setup_pose, const void *saved) {
 	const mbik::HostPlan &h = p->host;
 	CmodeState &c = p->cm;
 	c.W = std::max(1, (h.cm_npos + 31) / 32);
@@ -1468,6 +1506,13 @@ int cmode_create(mbik_plan *p, const float *setup_pose) {
 	c.node = static_cast<float *>(a);
 	c.dirty = static_cast<uint32_t *>(d);
 	if (N == 0) return MBIK_OK;
+	if (saved) { // mbik_plan_load: the saved frame-to-frame node caches
+		const char *sv = static_cast<const char *>(saved);
+		if (hipMemcpy(a, sv, node_bytes, hipMemcpyHostToDevice) != hipSuccess ||
+				hipMemcpy(d, sv + node_bytes, dirty_bytes, hipMemcpyHostToDevice) != hipSuccess)
+			return fail(MBIK_EHIP, "hipMemcpy constraint_mode state");
+		return MBIK_OK;
+	}
 	const size_t pose_bytes = N * h.B * 10 * sizeof(float);
 	if (hipMalloc(&sp, pose_bytes) != hipSuccess) return fail(MBIK_ENOMEM, "hipMalloc setup pose");
 	rc = hipMemcpy(sp, setup_pose, pose_bytes, hipMemcpyHostToDevice) == hipSuccess ? MBIK_OK : fail(MBIK_EHIP, "hipMemcpy setup pose");
@@ -1525,6 +1570,11 @@ int launch(mbik_plan *p, int first, int count, const float *pose_in, const float
 
 } // namespace
 
+namespace {
+void keep_inputs(mbik_plan *p, const mbik_skeleton_desc &desc, const mbik_config &cfg);
+int finish_plan(mbik_plan *p, const float *setup_pose, const void *cm_state);
+} // namespace
+
 extern "C" {
 
 const char *mbik_last_error(void) { return g_err.c_str(); }
@@ -1555,10 +1605,38 @@ int32_t mbik_plan_create(const mbik_skeleton_desc *desc, const mbik_config *conf
 	if (device < 0 || device >= ndev) return fail(MBIK_EINVAL, "device index out of range");
 	std::unique_ptr<mbik_plan> p(new mbik_plan());
 	p->device = device;
+	if (desc->bone_count < 0 || desc->pin_count < 0 || desc->constraint_count < 0 || config->bone_damp_count < 0)
+		return fail(MBIK_EINVAL, "negative count");
+	keep_inputs(p.get(), *desc, *config);
 	std::string err = mbik::build_topology(*desc, *config, p->host);
 	if (!err.empty()) return fail(MBIK_EINVAL, err);
 	err = mbik::build_skeletons(p->host, n_skeletons, setup_pose, cones, twist, std::max(1, desc->max_cones));
 	if (!err.empty()) return fail(MBIK_EINVAL, err);
+	const int rc = finish_plan(p.get(), setup_pose, nullptr);
+	if (rc) return rc;
+	*out_plan = p.release();
+	return MBIK_OK;
+}
+
+} // extern "C"
+namespace {
+void keep_inputs(mbik_plan *p, const mbik_skeleton_desc &desc, const mbik_config &cfg) {
+	p->src_parents.assign(desc.parents, desc.parents + (desc.parents ? desc.bone_count : 0));
+	p->src_pins.assign(desc.pins, desc.pins + (desc.pins ? desc.pin_count : 0));
+	p->src_cons.assign(desc.constraints, desc.constraints + (desc.constraints ? desc.constraint_count : 0));
+	p->src_bone_damp.assign(cfg.bone_damp, cfg.bone_damp + (cfg.bone_damp ? cfg.bone_damp_count : 0));
+	p->src_max_cones = desc.max_cones;
+	p->src_cfg = cfg;
+	p->src_cfg.bone_damp = nullptr;
+}
+
+// The device side of a plan whose HostPlan holds the topology and the per-skeleton tables
+// (D / CF / CD): uploads them, builds the launch schedule, and the constraint_mode node caches
+// -- from the setup pose (a new plan), or copied from a saved plan's bytes (cm_state: node
+// caches then dirty words, as mbik_plan_save wrote them).
+int finish_plan(mbik_plan *p, const float *setup_pose, const void *cm_state) {
+	const int device = p->device;
+	const int n_skeletons = p->host.N;
 	for (int b = 0; b < p->host.B; b++)
 		if ((p->host.bone_flags[b] & mbik::BF_PINNED) && p->host.bone_pin[b] >= 0) {
 			int e = p->host.bone_pin[b];
@@ -1578,18 +1656,21 @@ int32_t mbik_plan_create(const mbik_skeleton_desc *desc, const mbik_config *conf
 	d.n_gck = h.n_gck;
 	d.lds_stride = (mbik::lds_floats_per_skeleton(h) + 3) & ~3;
 	int rc = 0;
-	rc = rc ? rc : upload(p.get(), h.D, d.D);
-	rc = rc ? rc : upload(p.get(), h.CF, d.CF);
-	rc = rc ? rc : upload(p.get(), h.CD, d.CD);
+	rc = rc ? rc : upload(p, h.D, d.D);
+	rc = rc ? rc : upload(p, h.CF, d.CF);
+	rc = rc ? rc : upload(p, h.CD, d.CD);
 	if (rc) {
 		for (void *a : p->allocs) (void)hipFree(a);
+		p->allocs.clear();
 		return rc;
 	}
-	rc = ensure_schedule(p.get(), n_skeletons);
-	if (rc == 0 && h.constraint_mode) rc = cmode_create(p.get(), setup_pose);
+	rc = ensure_schedule(p, n_skeletons);
+	if (rc == 0 && h.constraint_mode) rc = cmode_create(p, setup_pose, cm_state);
 	if (rc) {
 		for (void *a : p->allocs) (void)hipFree(a);
+		p->allocs.clear();
 		if (p->d_sched) (void)hipFree(p->d_sched);
+		p->d_sched = nullptr;
 		return rc;
 	}
 	// Algorithmic HBM bytes per skeleton, each byte the solve needs read once and each
@@ -1625,6 +1706,186 @@ int32_t mbik_plan_create(const mbik_skeleton_desc *desc, const mbik_config *conf
 	h.D.clear(); h.D.shrink_to_fit();
 	h.CF.clear(); h.CF.shrink_to_fit();
 	h.CD.clear(); h.CD.shrink_to_fit();
+	return MBIK_OK;
+}
+} // namespace
+extern "C" {
+
+} // extern "C"
+// ---- plan serialisation (mbik_plan_save / mbik_plan_load) ----
+namespace {
+constexpr char kPlanMagic[8] = {'M', 'B', 'I', 'K', 'P', 'L', 'A', 'N'};
+constexpr uint32_t kPlanFormat = 1;
+struct PlanWriter {
+	std::vector<char> b;
+	void bytes(const void *v, size_t n) {
+		const char *c = static_cast<const char *>(v);
+		b.insert(b.end(), c, c + n);
+	}
+	template <class T>
+	void put(const T &v) { bytes(&v, sizeof(T)); }
+	template <class T>
+	void vec(const std::vector<T> &v) {
+		put<uint64_t>(v.size());
+		bytes(v.data(), v.size() * sizeof(T));
+	}
+};
+struct PlanReader {
+	const char *p, *e;
+	bool ok = true;
+	bool bytes(void *v, size_t n) {
+		if (!ok || (size_t)(e - p) < n) return ok = false;
+		std::memcpy(v, p, n);
+		p += n;
+		return true;
+	}
+	template <class T>
+	T get() {
+		T v{};
+		bytes(&v, sizeof(T));
+		return v;
+	}
+	template <class T>
+	std::vector<T> vec(uint64_t max_elems) {
+		const uint64_t n = get<uint64_t>();
+		std::vector<T> v;
+		if (!ok || n > max_elems || n > (uint64_t)(e - p) / sizeof(T)) {
+			ok = false;
+			return v;
+		}
+		v.resize(n);
+		bytes(v.data(), n * sizeof(T));
+		return v;
+	}
+};
+size_t cmode_state_bytes(const mbik_plan *p) {
+	const mbik::HostPlan &h = p->host;
+	return (size_t)(3 * h.B + 2 * h.NC) * 12 * (size_t)h.N * sizeof(float) + 4 * (size_t)p->cm.W * (size_t)h.N * sizeof(uint32_t);
+}
+} // namespace
+extern "C" {
+
+int32_t mbik_plan_save(const mbik_plan *p, void *buf, uint64_t capacity, uint64_t *size) {
+	if (!p || !size) return fail(MBIK_EINVAL, "null argument");
+	const mbik::HostPlan &h = p->host;
+	DeviceGuard guard(p->device);
+	// the device tables are read back: every stream that uses the plan must be idle
+	if (hipDeviceSynchronize() != hipSuccess) return fail(MBIK_EHIP, "hipDeviceSynchronize");
+	PlanWriter w;
+	w.bytes(kPlanMagic, sizeof(kPlanMagic));
+	w.put<uint32_t>(kPlanFormat);
+	w.put<uint32_t>(MBIK_ABI_VERSION);
+	w.put<int32_t>(h.N);
+	w.vec(p->src_parents);
+	w.vec(p->src_pins);
+	w.vec(p->src_cons);
+	w.put<int32_t>(p->src_max_cones);
+	w.put<int32_t>(p->src_cfg.iterations_per_frame);
+	w.put<float>(p->src_cfg.default_damp);
+	w.put<int32_t>(p->src_cfg.constraint_mode);
+	w.put<int32_t>(p->src_cfg.stabilization_passes);
+	w.vec(p->src_bone_damp);
+	w.put<int32_t>(h.setup_max_cones);
+	const size_t N = (size_t)h.N;
+	std::vector<float> D((size_t)h.B * 9 * N), CF((size_t)h.NC * h.cf_stride() * N);
+	std::vector<double> CD((size_t)h.NC * h.cd_stride() * N);
+	if ((!D.empty() && hipMemcpy(D.data(), p->dev.D, D.size() * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess) ||
+			(!CF.empty() && hipMemcpy(CF.data(), p->dev.CF, CF.size() * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess) ||
+			(!CD.empty() && hipMemcpy(CD.data(), p->dev.CD, CD.size() * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess))
+		return fail(MBIK_EHIP, "hipMemcpy plan tables");
+	w.vec(D);
+	w.vec(CF);
+	w.vec(CD);
+	for (int32_t v : {p->lanes_override, p->spw_override, p->interval_override, p->staging_override, p->locals_override,
+				 p->waves_override, p->cm_lanes})
+		w.put<int32_t>(v);
+	std::vector<char> cm;
+	if (h.constraint_mode && N) {
+		cm.resize(cmode_state_bytes(p));
+		const size_t node_bytes = (size_t)(3 * h.B + 2 * h.NC) * 12 * N * sizeof(float);
+		if (hipMemcpy(cm.data(), p->cm.node, node_bytes, hipMemcpyDeviceToHost) != hipSuccess ||
+				hipMemcpy(cm.data() + node_bytes, p->cm.dirty, cm.size() - node_bytes, hipMemcpyDeviceToHost) != hipSuccess)
+			return fail(MBIK_EHIP, "hipMemcpy constraint_mode state");
+	}
+	w.vec(cm);
+	*size = w.b.size();
+	if (!buf) return MBIK_OK;
+	if (capacity < w.b.size()) return fail(MBIK_EINVAL, "buffer smaller than the saved plan (see *size)");
+	std::memcpy(buf, w.b.data(), w.b.size());
+	return MBIK_OK;
+}
+
+int32_t mbik_plan_load(const void *buf, uint64_t size, int32_t device, mbik_plan **out_plan) {
+	if (!buf || !out_plan) return fail(MBIK_EINVAL, "null argument");
+	*out_plan = nullptr;
+	int ndev = 0;
+	if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(MBIK_ENODEV, "no HIP device visible");
+	if (device < 0 || device >= ndev) return fail(MBIK_EINVAL, "device index out of range");
+	PlanReader r{static_cast<const char *>(buf), static_cast<const char *>(buf) + size};
+	char magic[8];
+	if (!r.bytes(magic, 8) || std::memcmp(magic, kPlanMagic, 8) != 0) return fail(MBIK_EINVAL, "not a saved mbik plan");
+	if (r.get<uint32_t>() != kPlanFormat) return fail(MBIK_EUNSUPPORTED, "saved plan format version not supported");
+	(void)r.get<uint32_t>(); // the ABI version that wrote it (informational)
+	const int32_t N = r.get<int32_t>();
+	constexpr uint64_t kMax = 1ull << 34;
+	std::unique_ptr<mbik_plan> p(new mbik_plan());
+	p->device = device;
+	p->src_parents = r.vec<int32_t>(1 << 24);
+	p->src_pins = r.vec<mbik_pin>(1 << 24);
+	p->src_cons = r.vec<mbik_constraint>(1 << 24);
+	p->src_max_cones = r.get<int32_t>();
+	p->src_cfg.iterations_per_frame = r.get<int32_t>();
+	p->src_cfg.default_damp = r.get<float>();
+	p->src_cfg.constraint_mode = r.get<int32_t>();
+	p->src_cfg.stabilization_passes = r.get<int32_t>();
+	p->src_bone_damp = r.vec<float>(1 << 24);
+	const int32_t setup_max_cones = r.get<int32_t>();
+	std::vector<float> D = r.vec<float>(kMax), CF = r.vec<float>(kMax);
+	std::vector<double> CD = r.vec<double>(kMax);
+	int32_t ov[7];
+	for (int32_t &v : ov) v = r.get<int32_t>();
+	std::vector<char> cm = r.vec<char>(kMax);
+	if (!r.ok || N <= 0) return fail(MBIK_EINVAL, "truncated or corrupt saved plan");
+	mbik_skeleton_desc desc{};
+	desc.bone_count = (int32_t)p->src_parents.size();
+	desc.parents = p->src_parents.data();
+	desc.pin_count = (int32_t)p->src_pins.size();
+	desc.pins = p->src_pins.data();
+	desc.constraint_count = (int32_t)p->src_cons.size();
+	desc.constraints = p->src_cons.data();
+	desc.max_cones = p->src_max_cones;
+	mbik_config cfg = p->src_cfg;
+	cfg.bone_damp_count = (int32_t)p->src_bone_damp.size();
+	cfg.bone_damp = p->src_bone_damp.empty() ? nullptr : p->src_bone_damp.data();
+	p->src_cfg.bone_damp_count = cfg.bone_damp_count;
+	mbik::HostPlan &h = p->host;
+	std::string err = mbik::build_topology(desc, cfg, h);
+	if (!err.empty()) return fail(MBIK_EINVAL, "saved plan: " + err);
+	h.N = N;
+	const size_t n = (size_t)N;
+	if (D.size() != (size_t)h.B * 9 * n || CF.size() != (size_t)h.NC * h.cf_stride() * n ||
+			CD.size() != (size_t)h.NC * h.cd_stride() * n)
+		return fail(MBIK_EINVAL, "saved plan tables do not match its topology");
+	mbik::setup_tables(h);
+	h.setup_max_cones = std::max(1, setup_max_cones);
+	h.D = std::move(D);
+	h.CF = std::move(CF);
+	h.CD = std::move(CD);
+	p->lanes_override = ov[0];
+	p->spw_override = ov[1];
+	p->interval_override = ov[2];
+	p->staging_override = ov[3];
+	p->locals_override = ov[4];
+	p->waves_override = ov[5];
+	p->cm_lanes = ov[6];
+	if (h.constraint_mode) {
+		const int W = std::max(1, (h.cm_npos + 31) / 32);
+		const size_t want = (size_t)(3 * h.B + 2 * h.NC) * 12 * n * sizeof(float) + 4 * (size_t)W * n * sizeof(uint32_t);
+		if (cm.size() != want) return fail(MBIK_EINVAL, "saved constraint_mode state does not match its topology");
+	}
+	DeviceGuard guard(device);
+	const int rc = finish_plan(p.get(), nullptr, h.constraint_mode ? cm.data() : nullptr);
+	if (rc) return rc;
 	*out_plan = p.release();
 	return MBIK_OK;
 }

@@ -115,6 +115,30 @@ class Plan:
                    bone_damp=wl.bone_damp, stabilization_passes=stabilization_passes,
                    constraint_mode=constraint_mode)
 
+    def save(self) -> bytes:
+        """mbik_plan_save: the plan as a flat binary (topology inputs, setup tables, layout,
+        constraint_mode node caches)."""
+        size = C.c_uint64(0)
+        check(self._L.mbik_plan_save(self.h, None, 0, C.byref(size)))
+        buf = C.create_string_buffer(size.value)
+        check(self._L.mbik_plan_save(self.h, buf, size.value, C.byref(size)))
+        return buf.raw[: size.value]
+
+    @classmethod
+    def load(cls, data: bytes, device: int = 0) -> "Plan":
+        """mbik_plan_load: a plan rebuilt on `device` from Plan.save() bytes."""
+        L = _lib.load()
+        h = C.c_void_p()
+        check(L.mbik_plan_load(data, len(data), int(device), C.byref(h)))
+        self = cls.__new__(cls)
+        self._L = L
+        self.h = h
+        inf = self.info()
+        self.n, self.B, self.P = inf["skeleton_count"], inf["bone_count"], inf["pin_count"]
+        self._slots, self._cf_stride, self._cd_stride = inf["constraint_slots"], inf["cf_stride"], inf["cd_stride"]
+        self.iterations = None
+        return self
+
     def info(self) -> dict:
         inf = MbikPlanInfo()
         check(self._L.mbik_plan_get_info(self.h, C.byref(inf)))
