@@ -887,10 +887,8 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 	const int flags = t.bone_flags[b];
 	bool swung = false;
 	X3 Gbd_stale;
-#ifdef MBIK_GS_REUSE
 	B3 GsB = {};     // P.basis * Lb.basis after the swing check, reused by the twist if not swung
 	bool gs_ok = false;
-#endif
 #ifdef MBIK_ABLATE_SWING
 	if (false) {
 #else
@@ -898,10 +896,8 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 #endif
 		const int slot = t.bone_cons[b];
 		X3 Gs = P * Lb;
-#ifdef MBIK_GS_REUSE
 		GsB = Gs.b;
 		gs_ok = true;
-#endif
 		Gbd_stale.b = Gs.b * ld_soa_basis(t.D, b, 9, 0, t.N, s);
 		Gbd_stale.o = Gs.o;
 		X3 Gco = {P.b, xform(P, Lb.o)}; // constraint_orientation: (I, pose local origin) under the parent
@@ -932,13 +928,9 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 		float half_cos = soa(t.CF, slot, cs, mbik::CF_TWIST_COS, t.N, s);
 		B3 Tb = ld_soa_basis(t.CF, slot, cs, mbik::CF_TWIST_T, t.N, s);
 		B3 Gct = P.b * Tb;
-#ifdef MBIK_GS_REUSE
 		X3 Gs;
 		if (gs_ok && !swung) Gs.b = GsB;
 		else Gs.b = P.b * Lb.b;
-#else
-		X3 Gs = P * Lb;
-#endif
 		B3 gtc = Gct * from_quat(tcr);
 		B3 align = orthonormalized(inverse(gtc) * Gs.b);
 		Q sw, tw;
