@@ -19,6 +19,10 @@
 #endif
 
 namespace gd {
+#if !defined(__HIPCC__)
+using std::isfinite; // a plain C++ compiler (the sanitizer build, tools/san) puts them in std::
+using std::isnan;
+#endif
 
 constexpr double CMP_EPSILON = 0.00001;
 constexpr double PI = 3.1415926535897932384626433833;

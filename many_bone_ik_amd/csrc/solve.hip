@@ -334,7 +334,6 @@ __device__ __forceinline__ void effector_headings(const DevPlan &t, const EffPre
 		const int off = p.off;
 		const int de = p.de;
 		int d = t.bone_depth[b] + 1;
-#ifndef MBIK_PATH_UNROLL2
 		if (d <= de) {
 			// software-pipelined: the next path bone's local pose loads during this product
 			X3 Ln = L.ld(t.eff_path[off + d]);
@@ -345,22 +344,6 @@ __device__ __forceinline__ void effector_headings(const DevPlan &t, const EffPre
 			}
 			X = X * Ln;
 		}
-#else
-		if (d <= de) {
-			// software-pipelined: the next path bone's local pose loads during this product.
-			// Two load buffers alternate (unrolled by two), so no loop-carried register copy
-			// of the pending transform is needed.
-			X3 La = L.ld(t.eff_path[off + d]), Lb;
-			for (;;) {
-				if (d < de) Lb = L.ld(t.eff_path[off + d + 1]);
-				X = X * La;
-				if (++d > de) break;
-				if (d < de) La = L.ld(t.eff_path[off + d + 1]);
-				X = X * Lb;
-				if (++d > de) break;
-			}
-		}
-#endif
 		E.b = X.b * p.Db;
 		E.o = X.o;
 	}
