@@ -1799,7 +1799,9 @@ int32_t mbik_plan_load(const void *buf, uint64_t size, int32_t device, mbik_plan
 	PlanReader r{static_cast<const char *>(buf), static_cast<const char *>(buf) + size};
 	char magic[8];
 	if (!r.bytes(magic, 8) || std::memcmp(magic, kPlanMagic, 8) != 0) return fail(MBIK_EINVAL, "not a saved mbik plan");
-	if (r.get<uint32_t>() != kPlanFormat) return fail(MBIK_EUNSUPPORTED, "saved plan format version not supported");
+	const uint32_t format = r.get<uint32_t>();
+	if (!r.ok) return fail(MBIK_EINVAL, "truncated or corrupt saved plan");
+	if (format != kPlanFormat) return fail(MBIK_EUNSUPPORTED, "saved plan format version not supported");
 	(void)r.get<uint32_t>(); // the ABI version that wrote it (informational)
 	const int32_t N = r.get<int32_t>();
 	constexpr uint64_t kMax = 1ull << 34;
