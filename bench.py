@@ -270,11 +270,13 @@ def main():
     # no suffix): a constraint_mode or stabilization run never borrows the plain kernel's
     key = f"c{cfg}_{n}" + ("_cmode" if args.constraint_mode else "") + \
         (f"_stab{args.stabilization_passes}" if args.stabilization_passes else "")
+    # the PMC traffic of exactly the layout timed here (autotune may pick differently per box)
+    tkey = key + "_" + layout_key(info)
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
-            if key in tj:
-                traffic = tj[key]["hbm_bytes_per_launch"]
+            if tkey in tj:
+                traffic = tj[tkey]["hbm_bytes_per_launch"]
         except Exception:
             traffic = None
     issue = None  # the single-wave VALU issue ceiling, from the committed PMC passes
@@ -312,7 +314,7 @@ def main():
                                                    "waves_per_simd")},
                    "parallelism": f"dp{world} (skeleton shards, no data-path collective)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_key": tkey,
                      "algorithmic_bytes_per_launch": alg_bytes, "kernel_ms": kernel_ms,
                      "note": "latency/VALU-bound serial chain; HBM fraction reported as requested (DESIGN.md §5)"},
         "valu": {"achieved": alg_flops / (kernel_ms * 1e-3) / 1e12, "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -333,6 +335,12 @@ def main():
     print(json.dumps(out))
     if dist:
         dist.destroy_process_group()
+
+
+def layout_key(info: dict) -> str:
+    """The launch layout a plan runs (mbik_plan_info), as the suffix of profiles/traffic.json keys."""
+    return (f"K{info['lanes_per_skeleton']}_s{info['skeletons_per_block']}_i{info['checkpoint_interval']}"
+            f"_st{info['heading_staging']}_pl{info['state_placement']}_w{info['waves_per_simd']}")
 
 
 def batch_shard(args, world: int, rank: int):

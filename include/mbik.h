@@ -177,7 +177,9 @@ int32_t mbik_plan_resident_blocks(const mbik_plan *plan, int64_t lds_bytes_per_b
  * interval, heading staging, state placement and waves per SIMD; dimensions pinned by the
  * setters above (a value other than 0 / -1) are kept.  A launch that is fully resident at the
  * default layout is left as it is (one skeleton's chain bounds it).  Runs the solve several
- * times from pose_in into pose_out (identical results); the two buffers must not overlap
+ * times from pose_in into pose_out (identical results); candidates within 1.5 % of the fastest
+ * count as tied and the earliest in the candidate order wins, so that timing noise does not
+ * change the pick from box to box; the two buffers must not overlap
  * (MBIK_EINVAL otherwise).  Synchronizes hip_stream.  The chosen layout is
  * fixed afterwards; mbik_plan_set_layout(plan, 0, 0, 0) and the staging / placement / waves
  * setters with -1 return to the defaults. */

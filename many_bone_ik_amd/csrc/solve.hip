@@ -2160,6 +2160,11 @@ int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const flo
 	float best_ms = 0.0f;
 	int best_spw = 0, best_c = 0, best_stg = 1, best_lh = 0, best_ln = lanes, best_wv = 1, rc = MBIK_OK;
 	std::vector<std::tuple<int, int, int, int, int, int>> seen; // resolved (K, spw, interval, staging, locals, waves)
+	struct Timed {
+		float ms;
+		int spw, interval, stg, lh, ln, wv;
+	};
+	std::vector<Timed> timed;
 	for (auto [spw, c, stg, lh, ln, wv] : cands) {
 		p->spw_override = spw;
 		p->interval_override = c;
@@ -2183,19 +2188,27 @@ int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const flo
 		}
 		float ms = 0.0f;
 		(void)hipEventElapsedTime(&ms, e0, e1);
+		timed.push_back({ms, p->host.spw, p->host.g_interval, stg, lh, ln, wv});
 		if (best_c == 0 || ms < best_ms) {
 			best_ms = ms;
-			best_spw = p->host.spw;
 			best_c = p->host.g_interval;
-			best_stg = stg;
-			best_lh = lh;
-			best_ln = ln;
-			best_wv = wv;
 		}
 	}
 	(void)hipEventDestroy(e0);
 	(void)hipEventDestroy(e1);
 	if (rc != MBIK_OK) return rc;
+	// Near-ties go to the earliest candidate (a fixed order), not to run-to-run timing noise
+	// (~1 %), so that boxes agree on the layout and per-layout evidence stays comparable.
+	for (const Timed &c : timed)
+		if (c.ms <= best_ms * 1.015f) {
+			best_spw = c.spw;
+			best_c = c.interval;
+			best_stg = c.stg;
+			best_lh = c.lh;
+			best_ln = c.ln;
+			best_wv = c.wv;
+			break;
+		}
 	p->spw_override = best_spw;
 	p->interval_override = best_c;
 	p->staging_override = best_stg;

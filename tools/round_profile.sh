@@ -13,9 +13,13 @@ B="$ROOT/bench.py --config $CFG --steps 20 --warmup 3 --no-cpu-baseline --no-par
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/ktrace -o run --output-format csv -- python3 $B > $OUT/ktrace.json 2> $OUT/ktrace.log
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o run --output-format csv -- python3 $B > $OUT/fetch.json 2> $OUT/fetch.log
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o run --output-format csv -- python3 $B > $OUT/write.json 2> $OUT/write.log
-N=$(python3 -c "import json,sys; print(json.loads(open('$OUT/ktrace.json').read().strip().splitlines()[-1])['config']['skeletons_per_gpu'])")
+# keyed by config, size and the layout the PMC runs' autotune picked (bench.py reads the key of
+# the layout it times); a pass whose layout differs from the kernel-trace run's is reported
+KEY=$(python3 -c "import json; d=json.loads(open('$OUT/fetch.json').read().strip().splitlines()[-1]); print(d['roofline']['traffic_key'])")
+KEYW=$(python3 -c "import json; d=json.loads(open('$OUT/write.json').read().strip().splitlines()[-1]); print(d['roofline']['traffic_key'])")
+[ "$KEY" = "$KEYW" ] || { echo "FETCH and WRITE passes picked different layouts: $KEY vs $KEYW"; exit 3; }
 # the last 26 dispatches: 20 timed steps + 6 host-buffer frames, after autotune fixed the layout
-python3 tools/traffic_from_pmc.py $(ls $OUT/fetch/run_counter_collection.csv) $(ls $OUT/write/run_counter_collection.csv) c${CFG}_$N profiles/traffic.json --last 26
+python3 tools/traffic_from_pmc.py $(ls $OUT/fetch/run_counter_collection.csv) $(ls $OUT/write/run_counter_collection.csv) $KEY profiles/traffic.json --last 26
 cp profiles/traffic.json $OUT/traffic.json
 timeout -k 10 300 python3 bench.py --config $CFG > $OUT/bench.json 2> $OUT/bench.err
 cat $OUT/bench.json
