@@ -56,6 +56,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-autotune", action="store_true", help="keep the plan's automatic launch layout")
+    ap.add_argument("--layout", default="",
+                    help="pin a launch layout instead of autotuning: K:spw:interval:staging:placement:waves "
+                         "(mbik_plan_info's fields; tools/round_profile.sh passes the one its first run picked)")
     ap.add_argument("--constraint-mode", action="store_true",
                     help="ManyBoneIK3D::constraint_mode (snaps only; each step is one frame of the persistent node caches)")
     ap.add_argument("--stabilization-passes", type=int, default=0)
@@ -169,7 +172,15 @@ def main():
     def step():
         plan.solve(pose_in.data_ptr(), targets.data_ptr(), pose_out.data_ptr(), 0, n, stream.cuda_stream)
 
-    if not args.no_autotune:
+    if args.layout:
+        k, spw, interval, staging, placement, waves = (int(x) for x in args.layout.split(":"))
+        plan.set_layout(k, spw, interval)
+        plan.set_heading_staging(staging)
+        plan.set_locals_placement(placement)
+        plan.set_waves_per_simd(waves)
+        step()
+        info = plan.info()
+    elif not args.no_autotune:
         # mbik_plan_autotune: times the candidate launch layouts on this very batch and keeps
         # the fastest (every layout computes identical bits); part of warmup, not timed.
         plan.autotune(pose_in.data_ptr(), targets.data_ptr(), pose_out.data_ptr(), 0, n, stream.cuda_stream)

@@ -11,6 +11,9 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 B="$ROOT/bench.py --config $CFG --steps 20 --warmup 3 --no-cpu-baseline --no-parity"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/ktrace -o run --output-format csv -- python3 $B > $OUT/ktrace.json 2> $OUT/ktrace.log
+# the PMC passes and the final bench line run the layout the kernel-trace run's autotune picked
+LAYOUT=$(python3 -c "import json; c=json.loads(open('$OUT/ktrace.json').read().strip().splitlines()[-1])['config']; l=c['layout']; print(':'.join(str(x) for x in (c['lanes_per_skeleton'], c['skeletons_per_block'], l['checkpoint_interval'], l['heading_staging'], l['state_placement'], l['waves_per_simd'])))")
+B="$B --layout $LAYOUT"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o run --output-format csv -- python3 $B > $OUT/fetch.json 2> $OUT/fetch.log
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o run --output-format csv -- python3 $B > $OUT/write.json 2> $OUT/write.log
 # keyed by config, size and the layout the PMC runs' autotune picked (bench.py reads the key of
@@ -21,5 +24,5 @@ KEYW=$(python3 -c "import json; d=json.loads(open('$OUT/write.json').read().stri
 # the last 26 dispatches: 20 timed steps + 6 host-buffer frames, after autotune fixed the layout
 python3 tools/traffic_from_pmc.py $(ls $OUT/fetch/run_counter_collection.csv) $(ls $OUT/write/run_counter_collection.csv) $KEY profiles/traffic.json --last 26
 cp profiles/traffic.json $OUT/traffic.json
-timeout -k 10 300 python3 bench.py --config $CFG > $OUT/bench.json 2> $OUT/bench.err
+timeout -k 10 300 python3 bench.py --config $CFG --layout $LAYOUT > $OUT/bench.json 2> $OUT/bench.err
 cat $OUT/bench.json
