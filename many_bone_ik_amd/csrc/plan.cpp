@@ -116,6 +116,7 @@ std::string build_topology(const mbik_skeleton_desc &desc, const mbik_config &cf
 		gen(root_segs.back());
 	}
 	if (root_segs.empty()) return "skeleton has no parentless bone";
+	if (B > 32767 || p.P > 32767) return "more than 32767 bones or pins (the solve's step records hold 16-bit fields)";
 
 	// Kept segments in solve (post-order) numbering; bone_list per create_bone_list(true).
 	std::vector<int> order; // old ids in post-order
@@ -443,13 +444,15 @@ int32_t state_floats_per_skeleton(const HostPlan &p) {
 int64_t topology_bytes(const HostPlan &p) {
 	int64_t w = 4 * (int64_t)p.sched.size() + 4;
 	auto ints = [&](size_t n) { w += (int64_t)std::max<size_t>(n, 1) + 1; };
-	ints(p.bone_pose_parent.size()); ints(p.bone_depth.size()); ints(p.bone_flags.size()); ints(p.bone_pin.size());
-	ints(p.bone_cons.size()); ints(p.bone_child_eff_off.size()); ints(p.bone_child_effs.size());
+	// the tables MBIK_TOPO_TABLES lists (solve.hip), in its order
+	ints(p.bone_pose_parent.size()); ints(p.bone_flags.size()); ints(p.bone_pin.size());
+	ints(p.bone_cons.size()); ints(p.bone_child_effs.size());
 	ints(p.seg_bone_off.size()); ints(p.seg_bones.size()); ints(p.seg_eff_off.size()); ints(p.seg_effs.size());
 	ints(p.seg_eff_hoff.size()); ints(p.seg_nh.size()); ints(p.seg_flags.size()); ints(p.seg_hw_off.size());
-	ints(p.seg_wsum2.size()); ints(p.seg_hbase.size()); ints(p.B); ints(p.seg_bones.size());
+	ints(p.seg_wsum2.size()); ints(p.seg_hbase.size()); ints(p.B);
 	ints(p.eff_bone.size()); ints(p.eff_path_off.size()); ints(p.eff_path.size()); ints(p.eff_prio.size());
 	ints(p.cons_ncones.size()); ints(2 * p.seg_hw.size()); ints(2 * p.seg_cos_half_damp.size());
+	ints(4 * p.seg_bones.size() + 3); // step_rec, 16-byte aligned
 	return (w + 4) * 4;
 }
 
@@ -584,6 +587,18 @@ void build_schedule(HostPlan &p, int32_t lanes, int64_t nlaunch, int32_t spw_ove
 		}
 	}
 	set_interval(best_c);
+	p.step_rec.assign(4 * p.seg_bones.size(), 0);
+	for (size_t k = 0; k < p.seg_bones.size(); k++) {
+		const int b = p.seg_bones[k], pp = p.bone_pose_parent[b], kc = p.seg_anchor[k];
+		const int pslot = pp >= 0 ? p.bone_gslot[kc < 0 ? pp : p.seg_bones[kc]] : -1;
+		const int c0 = p.bone_child_eff_off[b], c1 = p.bone_child_eff_off[b + 1];
+		int32_t *r = &p.step_rec[4 * k];
+		r[0] = b | ((kc + 1) << 16);
+		r[1] = (pslot + 1) | ((p.bone_cons[b] + 1) << 16);
+		r[2] = p.bone_flags[b] | (pp != POSE_PARENT_NONE ? SR_HAS_POSE_PARENT : 0) | (pp >= 0 ? SR_PARENT_GLOBAL : 0) |
+				((p.bone_depth[b] + 1) << 16);
+		r[3] = c0 | ((c1 - c0) << 16);
+	}
 	p.spw = best;
 	p.lds_block_bytes = best * (int64_t)(((lds_floats_per_skeleton(p) + 3) & ~3) * 4) + topo;
 }

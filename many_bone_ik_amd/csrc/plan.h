@@ -18,6 +18,12 @@ enum BoneFlags : int32_t {
 	BF_PINNED = 8,     // carries an IKEffector3D
 };
 
+// Extra bits of a step record's flags word (HostPlan::step_rec).
+enum StepRecBits : int32_t {
+	SR_HAS_POSE_PARENT = 1 << 8,   // bone_pose_parent != POSE_PARENT_NONE (parented, maybe by the origin)
+	SR_PARENT_GLOBAL = 1 << 9,     // bone_pose_parent >= 0: the parent's global is a G slot
+};
+
 enum SegFlags : int32_t {
 	SF_TRANSLATE = 1,  // root segment: translate=true, damp=PI (ik_bone_segment_3d.cpp:217-222)
 	SF_STAB = 2,       // root segment built with default_stabilizing_pass_count > 0 (many_bone_ik_3d.cpp:1046;
@@ -110,6 +116,11 @@ struct HostPlan {
 	int32_t g_interval = 1, n_gck = 0;
 	std::vector<int32_t> bone_gslot;                // LDS slot of a checkpoint bone, else -1
 	std::vector<int32_t> seg_anchor;                // per seg_bones index: the checkpoint's index, -1 = parent outside
+	// Per seg_bones index k, what a bone-step looks up, resolved into one 16-byte record (no
+	// dependent lookups), 16-bit fields: x = bone | (checkpoint index + 1) << 16; y = (G slot of
+	// the parent's global or of its checkpoint, + 1) | (constraint slot + 1) << 16; z = bone
+	// flags | SR_* bits | path start (depth + 1) << 16; w = child-effector offset | count << 16.
+	std::vector<int32_t> step_rec;
 	std::vector<SchedTask> sched;                   // [nrows][K]
 	int32_t nrows = 0;
 	// ---- per skeleton, SoA [item][field][N] ----

@@ -65,11 +65,12 @@ namespace {
 // in HBM and copied into LDS at kernel start, so the many small dependent lookups of a
 // bone-step (segment -> effector -> path -> bone) are LDS reads, not L2 round trips.
 #define MBIK_TOPO_TABLES(X)                                                                         \
-	X(int, bone_pose_parent) X(int, bone_depth) X(int, bone_flags) X(int, bone_pin) X(int, bone_cons)  \
-	X(int, bone_child_eff_off) X(int, bone_child_effs) X(int, seg_bone_off) X(int, seg_bones)         \
+	X(int, bone_pose_parent) X(int, bone_flags) X(int, bone_pin) X(int, bone_cons)                    \
+	X(int, bone_child_effs) X(int, seg_bone_off) X(int, seg_bones)                                    \
 	X(int, seg_eff_off) X(int, seg_effs) X(int, seg_eff_hoff) X(int, seg_nh) X(int, seg_flags)         \
 	X(int, seg_hw_off) X(int, eff_bone) X(int, eff_path_off) X(int, eff_path) X(float, eff_prio)       \
-	X(int, cons_ncones) X(float, seg_wsum2) X(int, seg_hbase) X(int, bone_gslot) X(int, seg_anchor) X(double, seg_hw) X(double, seg_cos_half_damp) X(int4, sched)
+	X(int, cons_ncones) X(float, seg_wsum2) X(int, seg_hbase) X(int, bone_gslot) X(double, seg_hw) X(double, seg_cos_half_damp) X(int4, sched) \
+	X(int4, step_rec)
 
 struct DevPlan {
 	int B, P, NS, NC, max_cones, nrows, K, log2K, spw, lds_stride;
@@ -323,7 +324,8 @@ __device__ __forceinline__ void heading_terms(const EffPre &p, const X3 &E, V3 o
 // headings' origin in OE; 2 take that origin from OE (target headings are built once per
 // bone-step, before the retry loop, while tip headings are rebuilt on every pass).
 template <class LV>
-__device__ __forceinline__ void effector_headings(const DevPlan &t, const EffPre &p, int b, const X3 &Gb, const LV &L,
+// d0: the path index of the solved bone's first descendant (its depth + 1, step record).
+__device__ __forceinline__ void effector_headings(const DevPlan &t, const EffPre &p, int d0, const X3 &Gb, const LV &L,
 		const float *ST, const int *SF, Headings &H, float *OE = nullptr, int oe_mode = 0) {
 	const int e = p.e;
 	X3 E;
@@ -333,7 +335,7 @@ __device__ __forceinline__ void effector_headings(const DevPlan &t, const EffPre
 		X3 X = Gb;
 		const int off = p.off;
 		const int de = p.de;
-		int d = t.bone_depth[b] + 1;
+		int d = d0;
 		if (d <= de) {
 			// software-pipelined: the next path bone's local pose loads during this product
 			X3 Ln = L.ld(t.eff_path[off + d]);
@@ -356,12 +358,12 @@ __device__ __forceinline__ void effector_headings(const DevPlan &t, const EffPre
 	heading_terms(p, E, oe, Gb.o, H);
 }
 template <class LV>
-__device__ __forceinline__ void effector_headings(const DevPlan &t, int e, int b, const X3 &Gb, const LV &L,
+__device__ __forceinline__ void effector_headings(const DevPlan &t, int e, int d0, const X3 &Gb, const LV &L,
 		const float *TG, const float *ST, const int *SF, size_t s, const double *hw, Headings &H, float *OE = nullptr,
 		int oe_mode = 0, const B3 *Db = nullptr) {
 	EffPre p;
 	load_eff(t, e, TG, s, hw, p, Db);
-	effector_headings(t, p, b, Gb, L, ST, SF, H, OE, oe_mode);
+	effector_headings(t, p, d0, Gb, L, ST, SF, H, OE, oe_mode);
 }
 
 // The heading pairs of effector p.e (ik_effector_3d.cpp:90-149): E = the effector bone's
@@ -545,20 +547,19 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 	uint64_t pt1 = pt0, pt3 = pt0;
 	const bool seg_translate = (t.seg_flags[seg] & mbik::SF_TRANSLATE) != 0;
 #endif
-	const int b = t.seg_bones[k];
-	const int pp = t.bone_pose_parent[b];
-	const bool hasP = pp != mbik::POSE_PARENT_NONE;
+	// the step's topology, resolved on the host (HostPlan::step_rec): no dependent lookups
+	const int4 sr = t.step_rec[k];
+	const int b = sr.x & 0xffff;
+	const int flags = sr.z & 0xffff;           // bone_flags | SR_* bits
+	const int d0 = sr.z >> 16;                 // path index of b's first descendant
+	const int slot = (sr.y >> 16) - 1;         // constraint slot
+	const bool hasP = (flags & mbik::SR_HAS_POSE_PARENT) != 0;
 	// The parent's iteration-start global: stored if the parent is a checkpoint, else rebuilt
 	// from the nearest checkpoint above it, with the global pass's own products.
 	X3 P = xid();
-	if (pp >= 0) {
-		const int kc = t.seg_anchor[k];
-		if (kc < 0) {
-			P = ld_x(G + 12 * t.bone_gslot[pp]);
-		} else {
-			P = ld_x(G + 12 * t.bone_gslot[t.seg_bones[kc]]);
-			for (int q = kc - 1; q > k; q--) P = P * L.ld(t.seg_bones[q]);
-		}
+	if (flags & mbik::SR_PARENT_GLOBAL) {
+		P = ld_x(G + 12 * ((sr.y & 0xffff) - 1));
+		for (int q = (sr.x >> 16) - 2; q > k; q--) P = P * L.ld(t.seg_bones[q]); // none when no checkpoint is skipped
 	}
 	const B3 Pinv = inverse(P.b);
 	const bool stab = STAB && (t.seg_flags[seg] & mbik::SF_STAB) != 0;
@@ -582,8 +583,8 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 	Headings H;
 	if (nh == 1) {
 		// one heading in the segment: every lane of the group computes it (qcp.cpp:59-78)
-		if (hoist) effector_headings(t, pre, b, Gb, L, ST, SF, H, OE, oe_mode);
-		else effector_headings(t, t.seg_effs[e0], b, Gb, L, TG, ST, SF, s, hw, H, OE, oe_mode, dbh ? &pre.Db : nullptr);
+		if (hoist) effector_headings(t, pre, d0, Gb, L, ST, SF, H, OE, oe_mode);
+		else effector_headings(t, t.seg_effs[e0], d0, Gb, L, TG, ST, SF, s, hw, H, OE, oe_mode, dbh ? &pre.Db : nullptr);
 		V3 mvd = H.hm[0], tgt = H.ht[0];
 		if (translate) {
 			double w = H.w[0];
@@ -608,8 +609,8 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 		if (translate) {
 			double wsum = 0;
 			for (int i = e0; i < e1; i++) {
-				if (hoist) effector_headings(t, pre, b, Gb, L, ST, SF, H, OE, oe_mode);
-				else effector_headings(t, t.seg_effs[i], b, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, oe_mode, dbh ? &pre.Db : nullptr);
+				if (hoist) effector_headings(t, pre, d0, Gb, L, ST, SF, H, OE, oe_mode);
+				else effector_headings(t, t.seg_effs[i], d0, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, oe_mode, dbh ? &pre.Db : nullptr);
 #pragma unroll
 				for (int h = 0; h < 7; h++) {
 					if (H.mask & (1 << h)) {
@@ -629,8 +630,8 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 		const V3 nmc = mc * -1.0f, ntc = tc * -1.0f;
 		for (int i = e0; i < e1; i++) {
 			MBIK_PROF_T(ph1);
-			if (hoist) effector_headings(t, pre, b, Gb, L, ST, SF, H, OE, oe_mode);
-			else effector_headings(t, t.seg_effs[i], b, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, oe_mode, dbh ? &pre.Db : nullptr);
+			if (hoist) effector_headings(t, pre, d0, Gb, L, ST, SF, H, OE, oe_mode);
+			else effector_headings(t, t.seg_effs[i], d0, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, oe_mode, dbh ? &pre.Db : nullptr);
 			MBIK_PROF_T(ph2);
 			MBIK_PROF_ADD(9, ph1, ph2);
 #pragma unroll
@@ -676,7 +677,7 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 		double *ex = reinterpret_cast<double *>(hsg + HS_REC * nh);
 		for (int i = e0 + j; i < e1; i += m) {
 			MBIK_PROF_T(ph1);
-			effector_headings(t, t.seg_effs[i], b, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, oe_mode);
+			effector_headings(t, t.seg_effs[i], d0, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, oe_mode);
 			MBIK_PROF_T(ph2);
 			MBIK_PROF_ADD(9, ph1, ph2);
 			float *r = hsg + HS_REC * t.seg_eff_hoff[i];
@@ -852,13 +853,13 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 	// bone-direction caches are refreshed from here on.
 	// Every lane of the group holds identical values, so each writes its own copy (same
 	// bytes) and later reads never depend on another lane's store ordering.
-	for (int c = t.bone_child_eff_off[b]; c < t.bone_child_eff_off[b + 1]; c++) SF[t.bone_child_effs[c]] = 0;
+	for (int c = sr.w & 0xffff, ce = c + (sr.w >> 16); c < ce; c++) SF[t.bone_child_effs[c]] = 0;
 	} else if (STAB && oe_mode == 1) {
 		// constraint_mode still builds the target headings before the loop (:135)
 		Headings H;
 		const double *hw = t.seg_hw + t.seg_hw_off[seg];
 		for (int i = t.seg_eff_off[seg] + j; i < t.seg_eff_off[seg + 1]; i += m)
-			effector_headings(t, t.seg_effs[i], b, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, 1);
+			effector_headings(t, t.seg_effs[i], d0, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, 1);
 	}
 
 	MBIK_PROF_T(pt2);
@@ -867,7 +868,6 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 	if (seg_translate) MBIK_PROF_ADD(17, pt1, pt2);
 #endif
 	// ---- Kusudama: orientation (swing) snap (ik_kusudama_3d.cpp:347-376) ----
-	const int flags = t.bone_flags[b];
 	bool swung = false;
 	X3 Gbd_stale;
 	B3 GsB = {};     // P.basis * Lb.basis after the swing check, reused by the twist if not swung
@@ -877,7 +877,6 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 #else
 	if (flags & mbik::BF_ORIENT) {
 #endif
-		const int slot = t.bone_cons[b];
 		X3 Gs = P * Lb;
 		GsB = Gs.b;
 		gs_ok = true;
@@ -904,7 +903,6 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 #else
 	if (flags & mbik::BF_AXIAL) {
 #endif
-		const int slot = t.bone_cons[b];
 		const int cs = t.cf_stride;
 		Q tcr = q4(soa(t.CF, slot, cs, mbik::CF_TWIST_Q, t.N, s), soa(t.CF, slot, cs, mbik::CF_TWIST_Q + 1, t.N, s),
 				soa(t.CF, slot, cs, mbik::CF_TWIST_Q + 2, t.N, s), soa(t.CF, slot, cs, mbik::CF_TWIST_Q + 3, t.N, s));
@@ -944,7 +942,7 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 		Headings H;
 		for (int i = t.seg_eff_off[seg] + j; i < t.seg_eff_off[seg + 1]; i += m) {
 			const int e = t.seg_effs[i];
-			effector_headings(t, e, b, Gnow, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, 2);
+			effector_headings(t, e, d0, Gnow, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, 2);
 #pragma unroll
 			for (int h = 0; h < 7; h++) {
 				if (H.mask & (1 << h)) {
@@ -976,7 +974,7 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 		if (!eq(Lb, Lprev)) {
 			L.st(b, Lprev);
 			if (flags & mbik::BF_PINNED) SF[t.bone_pin[b]] = 0;
-			for (int c = t.bone_child_eff_off[b]; c < t.bone_child_eff_off[b + 1]; c++) SF[t.bone_child_effs[c]] = 0;
+			for (int c = sr.w & 0xffff, ce = c + (sr.w >> 16); c < ce; c++) SF[t.bone_child_effs[c]] = 0;
 		}
 		wave_sync_lds();
 		if (attempt + 1 >= t.stab) break;
@@ -1332,7 +1330,7 @@ int upload_topology(mbik_plan *p) {
 	for (size_t i = 0; i < rows.size(); i++) rows[i] = make_int4(h.sched[i].seg, h.sched[i].j, h.sched[i].m, 0);
 	add(rows.data(), rows.size() * sizeof(int4), 4, d.o_sched);
 #define MBIK_ADD(T, name) \
-	if (std::string(#name) != "sched") add(h.name.data(), h.name.size() * sizeof(h.name[0]), sizeof(T) >= 8 ? 2 : 1, d.o_##name);
+	if (std::string(#name) != "sched") add(h.name.data(), h.name.size() * sizeof(h.name[0]), sizeof(T) >= 16 ? 4 : (sizeof(T) >= 8 ? 2 : 1), d.o_##name);
 	MBIK_TOPO_TABLES(MBIK_ADD)
 #undef MBIK_ADD
 	while (blob.size() % 4) blob.push_back(0);
