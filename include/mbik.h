@@ -164,6 +164,27 @@ int32_t mbik_plan_set_waves_per_simd(mbik_plan *plan, int32_t waves);
  * result equals the host builder's.  Synchronizes hip_stream. */
 int32_t mbik_plan_rebuild_setup(mbik_plan *plan, int32_t first, int32_t count, const float *setup_pose,
 		const float *cones, const float *twist, void *hip_stream);
+/* GPU-side plan build for a crowd of distinct rigs: the segmentation, effector
+ * lists, heading weights (generate_default_segments ik_bone_segment_3d.cpp:352-427,
+ * update_pinned_list :74-88, create_headings_arrays / recursive_create_penalty_array
+ * :281-343), damping, effector paths and constraint slots of every rig are built on `device`,
+ * one GPU thread per rig (topo.h), and each rig's per-skeleton frames by mbik_setup_kernel
+ * from device buffers: setup_pose[i] [n_skeletons[i]][bones][10], cones[i] / twist[i] as for
+ * mbik_plan_rebuild_setup (NULL for rigs without constraints).  The host only reads the built
+ * tables back to size the launch layout; the damping cosines cos(damp/2) come from the host's
+ * libm (the reference's: the device's double cos differs in the last bit on ~1.6 % of inputs).
+ * out_plans[i] receives rig i's plan (equal to what mbik_plan_create builds from the same
+ * inputs); on error no plan is returned.  Combine them with mbik_group_create. */
+int32_t mbik_plan_create_device(int32_t n_rigs, const mbik_skeleton_desc *descs, const mbik_config *configs,
+		const int32_t *n_skeletons, const float *const *setup_pose, const float *const *cones, const float *const *twist,
+		int32_t device, mbik_plan **out_plans);
+/* Self-test of the GPU topology build: builds the n rigs with topo.h on `device` (or on the
+ * host when device < 0: the same code) and compares every topology table with the host
+ * builder's (mbik_plan_create's).  mismatches[i] = number of differing tables of rig i (0 when
+ * equal, also when both refuse the rig with the same error); mbik_last_error() names the
+ * first difference. */
+int32_t mbik_selftest_topology(int32_t n_rigs, const mbik_skeleton_desc *descs, const mbik_config *configs, int32_t device,
+		int32_t *mismatches);
 /* Copies the plan's per-skeleton setup tables to host buffers (any may be NULL):
  * D [bones][9][n], CF [slots][14 + 31*max_cones][n] floats, CD [slots][2*max_cones][n]
  * doubles, n = skeleton_count; slots = constraints on bones in the IK bone list

@@ -27,7 +27,7 @@ EXPORTED_SYMBOLS = (
     "mbik_plan_set_locals_placement", "mbik_plan_set_waves_per_simd", "mbik_plan_rebuild_setup", "mbik_plan_setup_tables",
     "mbik_solve", "mbik_solve_checked", "mbik_solve_host", "mbik_segment_solve", "mbik_plan_segment_table", "mbik_describe_topology",
     "mbik_group_create", "mbik_group_solve", "mbik_group_destroy", "mbik_capture_targets", "mbik_selftest_math",
-    "mbik_selftest_libm", "mbik_selftest_div", "mbik_last_error",
+    "mbik_selftest_libm", "mbik_selftest_div", "mbik_selftest_topology", "mbik_plan_create_device", "mbik_last_error",
 )
 
 
@@ -126,6 +126,11 @@ def load():
     L.mbik_solve_checked.restype = C.c_int32
     L.mbik_selftest_math.argtypes = [C.c_int32, C.POINTER(C.c_uint64)]
     L.mbik_selftest_math.restype = C.c_int32
+    L.mbik_selftest_topology.argtypes = [C.c_int32, vp, vp, C.c_int32, C.POINTER(C.c_int32)]
+    L.mbik_selftest_topology.restype = C.c_int32
+    L.mbik_plan_create_device.argtypes = [C.c_int32, vp, vp, C.POINTER(C.c_int32), C.POINTER(vp), C.POINTER(vp),
+                                          C.POINTER(vp), C.c_int32, C.POINTER(vp)]
+    L.mbik_plan_create_device.restype = C.c_int32
     L.mbik_selftest_div.argtypes = [C.c_int32, C.c_uint64, C.POINTER(C.c_uint64)]
     L.mbik_selftest_div.restype = C.c_int32
     L.mbik_selftest_libm.argtypes = [C.c_int32, C.c_uint64, C.c_uint64, vp, vp, C.POINTER(C.c_uint64), vp]
@@ -156,3 +161,8 @@ def check(rc: int) -> int:
     if rc < 0:
         raise MbikError(rc, load().mbik_last_error().decode(errors="replace"))
     return rc
+
+
+def last_error() -> str:
+    """mbik_last_error() of this thread."""
+    return load().mbik_last_error().decode(errors="replace")

@@ -6,6 +6,7 @@
 #include "plan.h"
 
 #include <algorithm>
+#include <type_traits>
 #include <cmath>
 #include <cstring>
 #include <functional>
@@ -14,6 +15,7 @@
 
 #include "gd_math.h"
 #include "setup.h"
+#include "topo.h"
 
 namespace mbik {
 
@@ -337,6 +339,122 @@ std::string build_topology(const mbik_skeleton_desc &desc, const mbik_config &cf
 	return "";
 }
 
+
+// ---------------------------------------------------------------------------------------
+// GPU-side topology build (topo.h): the host half
+// ---------------------------------------------------------------------------------------
+static double damp_cosine(float d) {
+	double dampening = (double)(float)(double)d; // float -> double -> float p_dampening -> double
+	return std::cos(dampening / 2.0);
+}
+void topology_damp_cosines(const mbik_skeleton_desc &desc, const mbik_config &cfg, std::vector<double> &bone_chd,
+		double &root_chd) {
+	bone_chd.assign(std::max(1, desc.bone_count), 0.0);
+	for (int b = 0; b < desc.bone_count; b++) { // build_topology's damping rule, per bone
+		float def = cfg.default_damp, d = def;
+		if (b < cfg.bone_damp_count && cfg.bone_damp) d = cfg.bone_damp[b];
+		if (def < d) d = def;
+		bone_chd[b] = damp_cosine(d);
+	}
+	root_chd = damp_cosine((float)gd::PI);
+}
+
+std::string assemble_topology(const TopoOut &o, const mbik_skeleton_desc &desc, const mbik_config &cfg, HostPlan &p) {
+	const int32_t *cnt = o.count;
+	if (cnt[TC_ERR]) return topo_error(cnt[TC_ERR]);
+	const int B = desc.bone_count, P = desc.pin_count;
+	const int NS = cnt[TC_NS];
+	auto v = [](const auto *a, int n) { return std::vector<std::remove_const_t<std::remove_pointer_t<decltype(a)>>>(a, a + n); };
+	p.B = B;
+	p.P = P;
+	p.max_cones = std::max(1, desc.max_cones);
+	p.iterations = cfg.iterations_per_frame;
+	p.constraint_mode = cfg.constraint_mode;
+	p.stabilization_passes = cfg.stabilization_passes;
+	p.parents.assign(desc.parents, desc.parents + B);
+	p.bone_depth = v(o.bone_depth, B);
+	p.bone_pin = v(o.bone_pin, B);
+	p.eff_bone.resize(P);
+	p.eff_prio.resize(3 * P);
+	for (int i = 0; i < P; i++) {
+		p.eff_bone[i] = desc.pins[i].bone;
+		for (int a = 0; a < 3; a++) p.eff_prio[3 * i + a] = desc.pins[i].direction_priorities[a];
+	}
+	p.bone_ik_parent = v(o.bone_ik_parent, B);
+	p.NS = NS;
+	p.seg_root = v(o.seg_root, NS);
+	p.seg_tip = v(o.seg_tip, NS);
+	p.seg_parent = v(o.seg_parent, NS);
+	p.seg_children.assign(NS, {});
+	for (int i = 0; i < NS; i++) p.seg_children[i] = v(o.seg_children + o.seg_child_off[i], o.seg_child_off[i + 1] - o.seg_child_off[i]);
+	p.seg_flags = v(o.seg_flags, NS);
+	p.seg_bone_off = v(o.seg_bone_off, NS + 1);
+	p.seg_bones = v(o.seg_bones, cnt[TC_NLIST]);
+	p.bone_list = v(o.bone_list, cnt[TC_NLIST]);
+	p.roots = v(o.roots, cnt[TC_NROOTS]);
+	p.bone_pose_parent = v(o.bone_pose_parent, B);
+	p.seg_eff_off = v(o.seg_eff_off, NS + 1);
+	p.seg_effs = v(o.seg_effs, cnt[TC_NSEGEFF]);
+	p.seg_eff_hoff = v(o.seg_eff_hoff, cnt[TC_NSEGEFF]);
+	p.seg_hw_off = v(o.seg_hw_off, NS);
+	p.seg_hw = v(o.seg_hw, cnt[TC_NHW]);
+	p.seg_nh = v(o.seg_nh, NS);
+	p.max_headings = cnt[TC_MAXH];
+	p.seg_wsum2 = v(o.seg_wsum2, NS);
+	p.seg_cos_half_damp = v(o.seg_cos_half_damp, cnt[TC_NLIST]);
+	p.eff_parent_bone = v(o.eff_parent_bone, P);
+	p.eff_path_off = v(o.eff_path_off, P + 1);
+	p.eff_path = v(o.eff_path, cnt[TC_NPATH]);
+	p.bone_flags = v(o.bone_flags, B);
+	p.bone_child_eff_off = v(o.bone_child_eff_off, B + 1);
+	p.bone_child_effs = v(o.bone_child_effs, cnt[TC_NCHILDEFF]);
+	p.bone_cons = v(o.bone_cons, B);
+	p.NC = cnt[TC_NC];
+	p.cons_bone = v(o.cons_bone, p.NC);
+	p.cons_ncones = v(o.cons_ncones, p.NC);
+	p.cons_order = v(o.cons_order, cnt[TC_NCONSORD]);
+	p.cons_order_slot = v(o.cons_order_slot, cnt[TC_NCONSORD]);
+	p.cons_order_ncones = v(o.cons_order_ncones, cnt[TC_NCONSORD]);
+	p.desc_constraint_count = desc.constraint_count;
+	p.seg_height = v(o.seg_height, NS);
+	p.seg_hbase.assign(NS, 0); // laid out by build_schedule
+	p.seg_tin = v(o.seg_tin, NS);
+	p.seg_tout = v(o.seg_tout, NS);
+	p.cm_pre = v(o.cm_pre, B);
+	p.cm_sub = v(o.cm_sub, B);
+	p.cm_maxd = cnt[TC_CM_MAXD];
+	p.cm_npos = cnt[TC_CM_NPOS];
+	return "";
+}
+
+int compare_topology(const HostPlan &a, const HostPlan &b, std::string *first) {
+	int n = 0;
+	auto note = [&](bool same, const char *name) {
+		if (same) return;
+		if (n++ == 0 && first) *first = name;
+	};
+	auto dbl_eq = [](const std::vector<double> &x, const std::vector<double> &y) {
+		return x.size() == y.size() && (x.empty() || std::memcmp(x.data(), y.data(), x.size() * sizeof(double)) == 0);
+	};
+	auto flt_eq = [](const std::vector<float> &x, const std::vector<float> &y) {
+		return x.size() == y.size() && (x.empty() || std::memcmp(x.data(), y.data(), x.size() * sizeof(float)) == 0);
+	};
+#define MBIK_CMP(f) note(a.f == b.f, #f);
+	MBIK_CMP(B) MBIK_CMP(P) MBIK_CMP(NS) MBIK_CMP(NC) MBIK_CMP(max_cones) MBIK_CMP(iterations) MBIK_CMP(constraint_mode)
+	MBIK_CMP(stabilization_passes) MBIK_CMP(parents) MBIK_CMP(bone_pose_parent) MBIK_CMP(bone_ik_parent) MBIK_CMP(bone_depth)
+	MBIK_CMP(bone_flags) MBIK_CMP(bone_pin) MBIK_CMP(bone_cons) MBIK_CMP(bone_list) MBIK_CMP(bone_child_eff_off)
+	MBIK_CMP(bone_child_effs) MBIK_CMP(seg_root) MBIK_CMP(seg_tip) MBIK_CMP(seg_parent) MBIK_CMP(seg_children)
+	MBIK_CMP(seg_bone_off) MBIK_CMP(seg_bones) MBIK_CMP(seg_eff_off) MBIK_CMP(seg_effs) MBIK_CMP(seg_eff_hoff) MBIK_CMP(seg_nh)
+	MBIK_CMP(seg_flags) MBIK_CMP(seg_hw_off) MBIK_CMP(seg_height) MBIK_CMP(seg_tin) MBIK_CMP(seg_tout) MBIK_CMP(roots)
+	MBIK_CMP(eff_bone) MBIK_CMP(eff_parent_bone) MBIK_CMP(eff_path_off) MBIK_CMP(eff_path) MBIK_CMP(eff_prio)
+	MBIK_CMP(cons_bone) MBIK_CMP(cons_ncones) MBIK_CMP(cons_order) MBIK_CMP(cons_order_slot) MBIK_CMP(cons_order_ncones)
+	MBIK_CMP(desc_constraint_count) MBIK_CMP(max_headings) MBIK_CMP(cm_pre) MBIK_CMP(cm_sub) MBIK_CMP(cm_maxd) MBIK_CMP(cm_npos)
+#undef MBIK_CMP
+	note(dbl_eq(a.seg_hw, b.seg_hw), "seg_hw");
+	note(dbl_eq(a.seg_cos_half_damp, b.seg_cos_half_damp), "seg_cos_half_damp");
+	note(flt_eq(a.seg_wsum2, b.seg_wsum2), "seg_wsum2");
+	return n;
+}
 
 // ---------------------------------------------------------------------------------------
 // Per-skeleton setup data

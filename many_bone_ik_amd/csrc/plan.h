@@ -135,6 +135,20 @@ struct HostPlan {
 
 // Builds the topology tables; returns an empty string on success, else the error.
 std::string build_topology(const mbik_skeleton_desc &desc, const mbik_config &cfg, HostPlan &plan);
+
+// The GPU-side topology build (topo.h), host half.
+struct TopoRig;
+struct TopoOut;
+// cos(damp/2) per bone of a non-root segment and of the root segments, as build_topology
+// evaluates them (the host libm's cos: the reference's), for TopoRig::bone_chd / root_chd.
+void topology_damp_cosines(const mbik_skeleton_desc &desc, const mbik_config &cfg, std::vector<double> &bone_chd,
+		double &root_chd);
+// A plan's topology from a topo_build result (o: host copies of the built tables), filled as
+// build_topology fills it.  Returns an empty string or the build's error.
+std::string assemble_topology(const TopoOut &o, const mbik_skeleton_desc &desc, const mbik_config &cfg, HostPlan &plan);
+// Number of topology tables that differ between two plans (0: identical), and the first
+// differing table's name.
+int compare_topology(const HostPlan &a, const HostPlan &b, std::string *first = nullptr);
 // Fills D / CF / CD for skeletons [0, n) from their setup poses, cones and twist.
 std::string build_skeletons(HostPlan &plan, int32_t n, const float *setup_pose, const float *cones, const float *twist,
 		int32_t max_cones_in);

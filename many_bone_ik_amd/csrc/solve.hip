@@ -37,6 +37,7 @@
 #include "gd_math.h"
 #include "plan.h"
 #include "setup.h"
+#include "topo.h"
 
 using namespace gd;
 
@@ -1239,6 +1240,24 @@ __global__ __launch_bounds__(64) void mbik_setup_kernel(mbik::SetupView v, int f
 		mbik::setup_skeleton(v, i, first + i, pose + (size_t)i * v.B * 10, cones, twist, w, D, CF, CD);
 }
 
+// GPU-side topology build (topo.h): one thread per rig, each with its own
+// output and scratch slices.
+struct TopoSlice {
+	mbik::TopoRig rig;
+	int32_t *out_i;
+	double *out_d;
+	float *out_f;
+	int32_t *scr_i;
+	double *scr_d;
+};
+__global__ __launch_bounds__(64) void mbik_topology_kernel(const TopoSlice *__restrict__ slices, int n) {
+	const int i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n) return;
+	const TopoSlice sl = slices[i];
+	const mbik::TopoRig &r = sl.rig;
+	mbik::topo_build(r, mbik::topo_out_at(sl.out_i, sl.out_d, sl.out_f, r.B, r.P, r.C), mbik::topo_scratch_at(sl.scr_i, sl.scr_d, r.B, r.P));
+}
+
 struct mbik_group {
 	std::vector<mbik_plan *> plans; // not owned
 	int device = 0;
@@ -1280,6 +1299,7 @@ struct mbik_plan {
 	std::vector<float> src_bone_damp;
 	int32_t src_max_cones = 1;
 	mbik_config src_cfg{};
+	bool setup_on_device = false; // mbik_plan_create_device: the setup pose given to finish_plan is a device buffer
 };
 
 namespace {
@@ -1486,6 +1506,11 @@ int cmode_create(mbik_plan *p, const float *setup_pose, const void *saved) {
 			return fail(MBIK_EHIP, "hipMemcpy constraint_mode state");
 		return MBIK_OK;
 	}
+	if (p->setup_on_device) { // mbik_plan_create_device: the setup pose already lives on the device
+		rc = cmode_reset(p, 0, (int)N, setup_pose, nullptr);
+		if (rc == 0 && hipDeviceSynchronize() != hipSuccess) rc = fail(MBIK_EHIP, "constraint_mode reset");
+		return rc;
+	}
 	const size_t pose_bytes = N * h.B * 10 * sizeof(float);
 	if (hipMalloc(&sp, pose_bytes) != hipSuccess) return fail(MBIK_ENOMEM, "hipMalloc setup pose");
 	rc = hipMemcpy(sp, setup_pose, pose_bytes, hipMemcpyHostToDevice) == hipSuccess ? MBIK_OK : fail(MBIK_EHIP, "hipMemcpy setup pose");
@@ -1683,6 +1708,231 @@ int finish_plan(mbik_plan *p, const float *setup_pose, const void *cm_state) {
 }
 } // namespace
 extern "C" {
+
+} // extern "C"
+// ---- GPU-side topology build (topo.h) ----
+namespace {
+// Builds the topologies of n rigs with topo.h -- on `device`, one GPU thread per rig, or on
+// the host when device < 0 (the same code; the CPU tests use it) -- and assembles each into
+// a HostPlan's topology.  errs[i] is the rig's error, empty when it built.
+int build_topologies(int n, const mbik_skeleton_desc *descs, const mbik_config *cfgs, int device,
+		std::vector<mbik::HostPlan> &out, std::vector<std::string> &errs) {
+	out.assign(n, mbik::HostPlan{});
+	errs.assign(n, std::string());
+	std::vector<mbik::TopoSizes> sz(n);
+	std::vector<size_t> in_i(n + 1, 0), in_f(n + 1, 0), in_d(n + 1, 0), o_i(n + 1, 0), o_d(n + 1, 0), o_f(n + 1, 0),
+			s_i(n + 1, 0), s_d(n + 1, 0);
+	std::vector<char> ok(n, 0);
+	for (int i = 0; i < n; i++) {
+		const mbik_skeleton_desc &d = descs[i];
+		const mbik_config &c = cfgs[i];
+		// build_topology's argument checks, in its order (the device never reads a bad pointer)
+		if (d.bone_count <= 0 || !d.parents) errs[i] = "bone_count must be > 0 and parents non-null";
+		else if (d.pin_count < 0 || (d.pin_count > 0 && !d.pins)) errs[i] = "invalid pins";
+		else if (d.constraint_count < 0 || (d.constraint_count > 0 && !d.constraints)) errs[i] = "invalid constraints";
+		else if (c.iterations_per_frame < 0) errs[i] = "iterations_per_frame must be >= 0";
+		ok[i] = errs[i].empty();
+		const int B = ok[i] ? d.bone_count : 1, P = ok[i] ? d.pin_count : 0, C = ok[i] ? d.constraint_count : 0;
+		sz[i] = mbik::topo_sizes(B, P, C);
+		in_i[i + 1] = in_i[i] + mbik::topo_align4((size_t)B + P + 2 * (size_t)C);
+		in_f[i + 1] = in_f[i] + mbik::topo_align4(5 * (size_t)P);
+		in_d[i + 1] = in_d[i] + mbik::topo_align4((size_t)B);
+		o_i[i + 1] = o_i[i] + sz[i].out_ints;
+		o_d[i + 1] = o_d[i] + sz[i].out_dbls;
+		o_f[i + 1] = o_f[i] + sz[i].out_flts;
+		s_i[i + 1] = s_i[i] + sz[i].scr_ints;
+		s_d[i + 1] = s_d[i] + sz[i].scr_dbls;
+	}
+	std::vector<int32_t> hin_i(in_i[n] + 4), hout_i(o_i[n] + 4);
+	std::vector<float> hin_f(in_f[n] + 4), hout_f(o_f[n] + 4);
+	std::vector<double> hin_d(in_d[n] + 4), hout_d(o_d[n] + 4);
+	std::vector<double> root_chd(n, 0.0);
+	for (int i = 0; i < n; i++) {
+		if (!ok[i]) continue;
+		const mbik_skeleton_desc &d = descs[i];
+		const int B = d.bone_count, P = d.pin_count, C = d.constraint_count;
+		int32_t *ii = hin_i.data() + in_i[i];
+		float *ff = hin_f.data() + in_f[i];
+		std::copy(d.parents, d.parents + B, ii);
+		for (int e = 0; e < P; e++) {
+			ii[B + e] = d.pins[e].bone;
+			ff[e] = d.pins[e].weight;
+			for (int a = 0; a < 3; a++) ff[P + 3 * e + a] = d.pins[e].direction_priorities[a];
+			ff[4 * P + e] = d.pins[e].motion_propagation_factor;
+		}
+		for (int c = 0; c < C; c++) {
+			ii[B + P + c] = d.constraints[c].bone;
+			ii[B + P + C + c] = d.constraints[c].cone_count;
+		}
+		std::vector<double> chd;
+		mbik::topology_damp_cosines(d, cfgs[i], chd, root_chd[i]);
+		std::copy(chd.begin(), chd.begin() + B, hin_d.data() + in_d[i]);
+	}
+	// the slices, pointing into device buffers (or into host buffers when device < 0)
+	char *dbase = nullptr;
+	std::vector<int32_t> hscr_i;
+	std::vector<double> hscr_d;
+	const size_t b_in_i = hin_i.size() * 4, b_in_f = hin_f.size() * 4, b_in_d = hin_d.size() * 8, b_o_i = hout_i.size() * 4,
+				 b_o_f = hout_f.size() * 4, b_o_d = hout_d.size() * 8, b_s_i = (s_i[n] + 4) * 4, b_s_d = (s_d[n] + 4) * 8,
+				 b_sl = (size_t)n * sizeof(TopoSlice);
+	auto a16 = [](size_t x) { return (x + 255) & ~size_t(255); };
+	const size_t off_in_f = a16(b_in_i), off_in_d = off_in_f + a16(b_in_f), off_o_i = off_in_d + a16(b_in_d),
+				 off_o_f = off_o_i + a16(b_o_i), off_o_d = off_o_f + a16(b_o_f), off_s_i = off_o_d + a16(b_o_d),
+				 off_s_d = off_s_i + a16(b_s_i), off_sl = off_s_d + a16(b_s_d), total = off_sl + a16(b_sl);
+	const bool on_device = device >= 0;
+	if (on_device) {
+		if (hipMalloc(&dbase, total) != hipSuccess) return fail(MBIK_ENOMEM, "hipMalloc topology build");
+	} else {
+		hscr_i.assign(s_i[n] + 4, 0);
+		hscr_d.assign(s_d[n] + 4, 0.0);
+	}
+	auto P_i = [&](size_t off, std::vector<int32_t> &h) { return on_device ? reinterpret_cast<int32_t *>(dbase + off) : h.data(); };
+	auto P_f = [&](size_t off, std::vector<float> &h) { return on_device ? reinterpret_cast<float *>(dbase + off) : h.data(); };
+	auto P_d = [&](size_t off, std::vector<double> &h) { return on_device ? reinterpret_cast<double *>(dbase + off) : h.data(); };
+	int32_t *bin_i = P_i(0, hin_i), *bout_i = P_i(off_o_i, hout_i), *bscr_i = P_i(off_s_i, hscr_i);
+	float *bin_f = P_f(off_in_f, hin_f), *bout_f = P_f(off_o_f, hout_f);
+	double *bin_d = P_d(off_in_d, hin_d), *bout_d = P_d(off_o_d, hout_d), *bscr_d = P_d(off_s_d, hscr_d);
+	std::vector<TopoSlice> slices(n);
+	for (int i = 0; i < n; i++) {
+		const mbik_skeleton_desc &d = descs[i];
+		const int B = ok[i] ? d.bone_count : 0, P = ok[i] ? d.pin_count : 0, C = ok[i] ? d.constraint_count : 0;
+		mbik::TopoRig &r = slices[i].rig;
+		r.B = B;
+		r.P = P;
+		r.C = C;
+		r.max_cones = d.max_cones;
+		r.stab = cfgs[i].stabilization_passes;
+		r.parents = bin_i + in_i[i];
+		r.pin_bone = bin_i + in_i[i] + B;
+		r.cons_bone = bin_i + in_i[i] + B + P;
+		r.cons_ncones = bin_i + in_i[i] + B + P + C;
+		r.pin_weight = bin_f + in_f[i];
+		r.pin_prio = bin_f + in_f[i] + P;
+		r.pin_mpf = bin_f + in_f[i] + 4 * P;
+		r.bone_chd = bin_d + in_d[i];
+		r.root_chd = root_chd[i];
+		slices[i].out_i = bout_i + o_i[i];
+		slices[i].out_d = bout_d + o_d[i];
+		slices[i].out_f = bout_f + o_f[i];
+		slices[i].scr_i = bscr_i + s_i[i];
+		slices[i].scr_d = bscr_d + s_d[i];
+	}
+	if (on_device) {
+		DeviceGuard guard(device);
+		int rc = MBIK_OK;
+		if (hipMemcpy(dbase, hin_i.data(), b_in_i, hipMemcpyHostToDevice) != hipSuccess ||
+				hipMemcpy(dbase + off_in_f, hin_f.data(), b_in_f, hipMemcpyHostToDevice) != hipSuccess ||
+				hipMemcpy(dbase + off_in_d, hin_d.data(), b_in_d, hipMemcpyHostToDevice) != hipSuccess ||
+				hipMemcpy(dbase + off_sl, slices.data(), b_sl, hipMemcpyHostToDevice) != hipSuccess)
+			rc = fail(MBIK_EHIP, "hipMemcpy topology inputs");
+		if (rc == MBIK_OK) {
+			hipLaunchKernelGGL(mbik_topology_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, 0,
+					reinterpret_cast<const TopoSlice *>(dbase + off_sl), n);
+			if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) rc = fail(MBIK_EHIP, "topology kernel");
+		}
+		if (rc == MBIK_OK && (hipMemcpy(hout_i.data(), dbase + off_o_i, b_o_i, hipMemcpyDeviceToHost) != hipSuccess ||
+								 hipMemcpy(hout_f.data(), dbase + off_o_f, b_o_f, hipMemcpyDeviceToHost) != hipSuccess ||
+								 hipMemcpy(hout_d.data(), dbase + off_o_d, b_o_d, hipMemcpyDeviceToHost) != hipSuccess))
+			rc = fail(MBIK_EHIP, "hipMemcpy topology outputs");
+		(void)hipFree(dbase);
+		if (rc) return rc;
+	} else {
+		for (int i = 0; i < n; i++) {
+			const mbik::TopoRig &r = slices[i].rig;
+			if (!ok[i]) continue;
+			mbik::topo_build(r, mbik::topo_out_at(slices[i].out_i, slices[i].out_d, slices[i].out_f, r.B, r.P, r.C),
+					mbik::topo_scratch_at(slices[i].scr_i, slices[i].scr_d, r.B, r.P));
+		}
+	}
+	for (int i = 0; i < n; i++) {
+		if (!ok[i]) continue;
+		const mbik_skeleton_desc &d = descs[i];
+		const mbik::TopoOut o = mbik::topo_out_at(hout_i.data() + o_i[i], hout_d.data() + o_d[i], hout_f.data() + o_f[i],
+				d.bone_count, d.pin_count, d.constraint_count);
+		errs[i] = mbik::assemble_topology(o, d, cfgs[i], out[i]);
+	}
+	return MBIK_OK;
+}
+} // namespace
+extern "C" {
+
+int32_t mbik_selftest_topology(int32_t n_rigs, const mbik_skeleton_desc *descs, const mbik_config *configs, int32_t device,
+		int32_t *mismatches) {
+	if (n_rigs < 0 || (n_rigs > 0 && (!descs || !configs || !mismatches))) return fail(MBIK_EINVAL, "null argument");
+	if (device >= 0) {
+		int ndev = 0;
+		if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(MBIK_ENODEV, "no HIP device visible");
+		if (device >= ndev) return fail(MBIK_EINVAL, "device index out of range");
+	}
+	std::vector<mbik::HostPlan> built;
+	std::vector<std::string> errs;
+	const int rc = build_topologies(n_rigs, descs, configs, device, built, errs);
+	if (rc) return rc;
+	std::string report;
+	for (int i = 0; i < n_rigs; i++) {
+		mbik::HostPlan ref;
+		const std::string rerr = mbik::build_topology(descs[i], configs[i], ref);
+		if (!rerr.empty() || !errs[i].empty()) {
+			// both must refuse the rig, with the same message
+			mismatches[i] = rerr == errs[i] ? 0 : 1;
+			if (mismatches[i] && report.empty()) report = "rig " + std::to_string(i) + ": '" + rerr + "' vs '" + errs[i] + "'";
+			continue;
+		}
+		std::string first;
+		mismatches[i] = mbik::compare_topology(ref, built[i], &first);
+		if (mismatches[i] && report.empty()) report = "rig " + std::to_string(i) + ": table " + first;
+	}
+	g_err = report;
+	return MBIK_OK;
+}
+
+int32_t mbik_plan_create_device(int32_t n_rigs, const mbik_skeleton_desc *descs, const mbik_config *configs,
+		const int32_t *n_skeletons, const float *const *setup_pose, const float *const *cones, const float *const *twist,
+		int32_t device, mbik_plan **out_plans) {
+	if (n_rigs <= 0 || !descs || !configs || !n_skeletons || !setup_pose || !out_plans) return fail(MBIK_EINVAL, "null argument");
+	for (int i = 0; i < n_rigs; i++) out_plans[i] = nullptr;
+	int ndev = 0;
+	if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(MBIK_ENODEV, "no HIP device visible");
+	if (device < 0 || device >= ndev) return fail(MBIK_EINVAL, "device index out of range");
+	for (int i = 0; i < n_rigs; i++)
+		if (n_skeletons[i] <= 0 || !setup_pose[i]) return fail(MBIK_EINVAL, "n_skeletons must be > 0 and setup_pose non-null");
+	std::vector<mbik::HostPlan> built;
+	std::vector<std::string> errs;
+	int rc = build_topologies(n_rigs, descs, configs, device, built, errs);
+	if (rc) return rc;
+	for (int i = 0; i < n_rigs; i++)
+		if (!errs[i].empty()) return fail(MBIK_EINVAL, "rig " + std::to_string(i) + ": " + errs[i]);
+	std::vector<std::unique_ptr<mbik_plan>> plans;
+	for (int i = 0; i < n_rigs && rc == MBIK_OK; i++) {
+		const mbik_skeleton_desc &d = descs[i];
+		std::unique_ptr<mbik_plan> p(new mbik_plan());
+		p->device = device;
+		p->setup_on_device = true;
+		keep_inputs(p.get(), d, configs[i]);
+		mbik::HostPlan &h = p->host;
+		h = std::move(built[i]);
+		for (int c : h.cons_order_ncones)
+			if (c > std::max(1, d.max_cones)) return fail(MBIK_EINVAL, "a constraint has more cones than max_cones");
+		if (h.NC > 0 && (!cones || !twist || !cones[i] || !twist[i]))
+			return fail(MBIK_EINVAL, "cones/twist required when constraints exist");
+		h.N = n_skeletons[i];
+		const size_t N = (size_t)h.N;
+		h.D.assign((size_t)h.B * 9 * N, 0.0f); // filled on the device below (mbik_setup_kernel)
+		h.CF.assign((size_t)h.NC * h.cf_stride() * N, 0.0f);
+		h.CD.assign((size_t)h.NC * h.cd_stride() * N, 0.0);
+		mbik::setup_tables(h);
+		h.setup_max_cones = std::max(1, d.max_cones);
+		if ((rc = finish_plan(p.get(), setup_pose[i], nullptr)) != MBIK_OK) break;
+		rc = mbik_plan_rebuild_setup(p.get(), 0, h.N, setup_pose[i], h.NC ? cones[i] : nullptr, h.NC ? twist[i] : nullptr, nullptr);
+		plans.push_back(std::move(p));
+	}
+	if (rc) {
+		for (auto &p : plans) mbik_plan_destroy(p.release());
+		return rc;
+	}
+	for (int i = 0; i < n_rigs; i++) out_plans[i] = plans[i].release();
+	return MBIK_OK;
+}
 
 } // extern "C"
 // ---- plan serialisation (mbik_plan_save / mbik_plan_load) ----

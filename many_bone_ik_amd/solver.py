@@ -73,6 +73,59 @@ def describe_topology(parents, pins, constraints=(), *, iterations=15, default_d
     return dict(bone_list=bl[:nbl.value], seg_root=r[:ns], seg_tip=t[:ns], seg_parent=p[:ns], seg_headings=nh[:ns])
 
 
+def _rig_arrays(rigs):
+    """ctypes arrays of descs / configs for (parents, pins, constraints, config-kwargs) rigs;
+    returns (descs, configs, keepalive)."""
+    keep = []
+    descs = (MbikSkeletonDesc * len(rigs))()
+    cfgs = (MbikConfig * len(rigs))()
+    for i, (parents, pins, constraints, kw) in enumerate(rigs):
+        constraints = list(constraints)
+        mc = kw.get("max_cones", max([1] + [int(c.get("cone_count", 0)) for c in constraints]))
+        d = _Desc(parents, pins, constraints, mc, kw.get("iterations", 15), kw.get("default_damp", math.radians(5.0)),
+                  kw.get("constraint_mode", False), kw.get("stabilization_passes", 0), kw.get("bone_damp"))
+        keep.append(d)
+        descs[i] = d.desc
+        cfgs[i] = d.cfg
+    return descs, cfgs, keep
+
+
+def topology_selftest(rigs, device: int = -1):
+    """mbik_selftest_topology: builds the rigs' topologies with the GPU builder's code (on the
+    host when device < 0) and compares every table with the host builder's.  Returns
+    (per-rig mismatching table counts, the first difference's description)."""
+    L = _lib.load()
+    descs, cfgs, keep = _rig_arrays(rigs)
+    out = (C.c_int32 * max(1, len(rigs)))()
+    check(L.mbik_selftest_topology(len(rigs), descs, cfgs, int(device), out))
+    return [int(out[i]) for i in range(len(rigs))], _lib.last_error()
+
+
+def plans_from_device(rigs, n_skeletons, setup_pose_ptrs, cones_ptrs=None, twist_ptrs=None, device: int = 0):
+    """mbik_plan_create_device: one Plan per rig, topology and setup built on the GPU from
+    device buffers (setup poses, cones, twist: device pointers, 0 / None where a rig has no
+    constraints)."""
+    L = _lib.load()
+    n = len(rigs)
+    descs, cfgs, keep = _rig_arrays(rigs)
+    vpa = C.c_void_p * n
+    out = vpa()
+    ptrs = lambda xs: vpa(*[(x or None) for x in (xs or [0] * n)])
+    check(L.mbik_plan_create_device(n, descs, cfgs, (C.c_int32 * n)(*n_skeletons), ptrs(setup_pose_ptrs), ptrs(cones_ptrs),
+                                    ptrs(twist_ptrs), int(device), out))
+    plans = []
+    for i, (parents, pins, constraints, kw) in enumerate(rigs):
+        p = Plan.__new__(Plan)
+        p._L = L
+        p.h = C.c_void_p(out[i])
+        inf = p.info()
+        p.n, p.B, p.P = inf["skeleton_count"], inf["bone_count"], inf["pin_count"]
+        p._slots, p._cf_stride, p._cd_stride = inf["constraint_slots"], inf["cf_stride"], inf["cd_stride"]
+        p.iterations = kw.get("iterations", 15)
+        plans.append(p)
+    return plans
+
+
 class Plan:
     """== ManyBoneIK3D after _bone_list_changed(), for a batch of same-topology skeletons."""
 
