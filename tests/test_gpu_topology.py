@@ -78,3 +78,12 @@ def test_device_plans_refuse_bad_rigs(mbik):
     with pytest.raises(_lib.MbikError) as e:
         plans_from_device([(np.array([1, 0], np.int32), [dict(bone=0)], [], {})], [1], [pose.data_ptr()])
     assert e.value.code == _lib.MBIK_EINVAL and "cycle" in str(e.value)
+
+
+def test_device_builder_on_a_large_random_crowd(mbik):
+    """2,048 random rigs (random trees, pins, priorities, weights, propagation factors,
+    constraints, damping, stabilization) built in one launch: every table as the host's."""
+    from .test_topology_build import random_rig
+    rigs = [random_rig(10_000 + s) for s in range(2048)]
+    mism, err = topology_selftest(rigs, device=0)
+    assert not any(mism), err
