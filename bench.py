@@ -293,7 +293,7 @@ def main():
     issue = None  # the single-wave VALU issue ceiling, from the committed PMC passes
     if os.path.exists(args.valu_mix_json):
         try:
-            vm = json.load(open(args.valu_mix_json)).get(key)
+            vm = json.load(open(args.valu_mix_json)).get(tkey)  # the mix of exactly this layout
             if vm:
                 issue = {"bound": "valu_issue_1wave", "achieved_cycles_per_wave": vm["valu_issue_floor_cycles"],
                          "wave_cycles": vm["wave_cycles"], "frac": vm["issue_frac"],

@@ -9,7 +9,7 @@ import subprocess
 import sys
 
 src, cfg = sys.argv[1], int(sys.argv[2])
-rnd = sys.argv[3] if len(sys.argv) > 3 else "r01"
+rnd = sys.argv[3] if len(sys.argv) > 3 else "r02"
 here = os.path.dirname(os.path.abspath(__file__))
 prof = os.path.join(here, "..", "profiles")
 c = f"c{cfg}"
@@ -21,7 +21,7 @@ shutil.copy(f"{src}/fetch/run_counter_collection.csv", f"{prof}/{rnd}_{c}_pmc_fe
 shutil.copy(f"{src}/write/run_counter_collection.csv", f"{prof}/{rnd}_{c}_pmc_write_size.csv")
 bench = json.loads(open(f"{src}/bench.json").read().strip().splitlines()[-1])
 t = json.load(open(f"{src}/traffic.json"))
-key = f"{c}_{bench['config']['skeletons_per_gpu']}"
+key = bench["roofline"]["traffic_key"]     # config, size and the layout timed
 tj_path = f"{prof}/traffic.json"
 tj = json.load(open(tj_path))
 tj[key] = t[key]
