@@ -26,8 +26,12 @@ tj_path = f"{prof}/traffic.json"
 tj = json.load(open(tj_path))
 tj[key] = t[key]
 json.dump(tj, open(tj_path, "w"), indent=1, sort_keys=True)
-vm = json.load(open(f"{prof}/valu_mix.json"))
-if key not in vm:
-    bench["issue"] = None  # no instruction-mix pass for this config's tuned layout
+vm = json.load(open(f"{prof}/valu_mix.json")).get(key)
+# the instruction-mix pass of this layout (tools/mix_entry.py), as bench.py reports it
+bench["issue"] = None if not vm else {
+    "bound": "valu_issue_1wave", "achieved_cycles_per_wave": vm["valu_issue_floor_cycles"],
+    "wave_cycles": vm["wave_cycles"], "frac": vm["issue_frac"],
+    "note": "4 cycles per wave64 VALU instruction x VALU instructions / wave cycles (PMC, "
+            "profiles/valu_mix.json); the ceiling this latency-bound chain runs against"}
 json.dump(bench, open(f"{prof}/{rnd}_{c}_bench.json", "w"))
 print(key, bench["ms_per_step"], bench["value"], bench["config"].get("layout"), json.loads(tail)["avg_ms"])
