@@ -144,7 +144,7 @@ struct CmodeLane {
 	// IKBone3D::get_bone_direction_global_pose (ik_bone_3d.cpp:157-159): local = (D, 0).
 	__device__ X3 bdir_global(int b) const {
 		if (!dirty(CK_BDIR, b)) return ld(GD(b));
-		const X3 G = pose_global(b) * X3{ld_soa_basis(t.D, b, 9, 0, t.N, s), v3(0, 0, 0)};
+		const X3 G = pose_global(b) * X3{ld_soa_basis(t, t.D, b, 9, 0, s), v3(0, 0, 0)};
 		st(GD(b), G);
 		set_clean(CK_BDIR, b);
 		return G;
@@ -165,7 +165,7 @@ struct CmodeLane {
 		const int k = GT(slot_);
 		if (!dirty(CK_CTW, b)) return ld(k);
 		const X3 G = pose_global(t.bone_pose_parent[b]) *
-				X3{ld_soa_basis(t.CF, slot_, t.cf_stride, mbik::CF_TWIST_T, t.N, s), v3(0, 0, 0)};
+				X3{ld_soa_basis(t, t.CF, slot_, t.cf_stride, mbik::CF_TWIST_T, s), v3(0, 0, 0)};
 		st(k, G);
 		set_clean(CK_CTW, b);
 		return G;
@@ -227,9 +227,9 @@ __device__ void cmode_step(const CmodeLane &C, int seg, int k, const float *tg, 
 			const X3 Gt = C.twist_global(b);
 			const X3 Gs = C.pose_global(b);
 			const B3 pgi = inverse(C.pose_global(t.bone_pose_parent[b]).b);
-			const Q tcr = q4(soa(t.CF, slot_, cs, mbik::CF_TWIST_Q, t.N, C.s), soa(t.CF, slot_, cs, mbik::CF_TWIST_Q + 1, t.N, C.s),
-					soa(t.CF, slot_, cs, mbik::CF_TWIST_Q + 2, t.N, C.s), soa(t.CF, slot_, cs, mbik::CF_TWIST_Q + 3, t.N, C.s));
-			const float half_cos = soa(t.CF, slot_, cs, mbik::CF_TWIST_COS, t.N, C.s);
+			const Q tcr = q4(soa(t, t.CF, slot_, cs, mbik::CF_TWIST_Q, C.s), soa(t, t.CF, slot_, cs, mbik::CF_TWIST_Q + 1, C.s),
+					soa(t, t.CF, slot_, cs, mbik::CF_TWIST_Q + 2, C.s), soa(t, t.CF, slot_, cs, mbik::CF_TWIST_Q + 3, C.s));
+			const float half_cos = soa(t, t.CF, slot_, cs, mbik::CF_TWIST_COS, C.s);
 			const B3 gtc = Gt.b * from_quat(tcr);
 			const B3 align = orthonormalized(inverse(gtc) * Gs.b);
 			Q sw, tw;

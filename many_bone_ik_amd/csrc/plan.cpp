@@ -571,6 +571,7 @@ int64_t topology_bytes(const HostPlan &p) {
 	ints(p.eff_bone.size()); ints(p.eff_path_off.size()); ints(p.eff_path.size()); ints(p.eff_prio.size());
 	ints(p.cons_ncones.size()); ints(2 * p.seg_hw.size()); ints(2 * p.seg_cos_half_damp.size());
 	ints(4 * p.seg_bones.size() + 3); // step_rec, 16-byte aligned
+	ints(p.seg_effs.size() + 1);      // seg_eff_lcp
 	return (w + 4) * 4;
 }
 
@@ -582,6 +583,15 @@ static int ceil_log2(int v) {
 
 void build_schedule(HostPlan &p, int32_t lanes, int64_t nlaunch, int32_t spw_override, int32_t interval_override,
 		BlocksPerCU blocks_per_cu, void *ctx, int cus) {
+	p.seg_eff_lcp.assign(p.seg_effs.size() + 1, 0);
+	for (int sg = 0; sg < p.NS; sg++)
+		for (int i = p.seg_eff_off[sg] + 1; i < p.seg_eff_off[sg + 1]; i++) {
+			const int a = p.seg_effs[i - 1], b = p.seg_effs[i];
+			const int la = p.eff_path_off[a + 1] - p.eff_path_off[a], lb = p.eff_path_off[b + 1] - p.eff_path_off[b];
+			int l = 0;
+			while (l < la && l < lb && p.eff_path[p.eff_path_off[a] + l] == p.eff_path[p.eff_path_off[b] + l]) l++;
+			p.seg_eff_lcp[i] = l;
+		}
 	int maxh = 0;
 	for (int i = 0; i < p.NS; i++) maxh = std::max(maxh, p.seg_height[i]);
 	std::vector<std::vector<int>> lev(maxh + 1);

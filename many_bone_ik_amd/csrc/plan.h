@@ -121,6 +121,10 @@ struct HostPlan {
 	// the parent's global or of its checkpoint, + 1) | (constraint slot + 1) << 16; z = bone
 	// flags | SR_* bits | path start (depth + 1) << 16; w = child-effector offset | count << 16.
 	std::vector<int32_t> step_rec;
+	// Per seg_effs index i: how many leading bones effector seg_effs[i]'s path (from the root)
+	// shares with the previous effector's of the same segment (0 for a segment's first), plus
+	// a trailing 0.  The solve reuses the previous effector's walk down to that depth.
+	std::vector<int32_t> seg_eff_lcp;
 	std::vector<SchedTask> sched;                   // [nrows][K]
 	int32_t nrows = 0;
 	// ---- per skeleton, SoA [item][field][N] ----

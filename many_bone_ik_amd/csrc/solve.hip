@@ -71,7 +71,7 @@ namespace {
 	X(int, seg_eff_off) X(int, seg_effs) X(int, seg_eff_hoff) X(int, seg_nh) X(int, seg_flags)         \
 	X(int, seg_hw_off) X(int, eff_bone) X(int, eff_path_off) X(int, eff_path) X(float, eff_prio)       \
 	X(int, cons_ncones) X(float, seg_wsum2) X(int, seg_hbase) X(int, bone_gslot) X(double, seg_hw) X(double, seg_cos_half_damp) X(int4, sched) \
-	X(int4, step_rec)
+	X(int4, step_rec) X(int, seg_eff_lcp)
 
 struct DevPlan {
 	int B, P, NS, NC, max_cones, nrows, K, log2K, spw, lds_stride;
@@ -87,6 +87,11 @@ struct DevPlan {
 #undef MBIK_DECL
 	const float *D, *CF;
 	const double *CD;
+	// The per-skeleton tables D / CF / CD are [item][field][N].  Launches with the whole state in
+	// device memory read a skeleton-tiled copy instead, [item][row_n/kRowTile][field][kRowTile]
+	// (row_n = N rounded up; row_at<true>): one lane group's skeletons x all fields of a slot
+	// are then whole cache lines.
+	int row_n = 0;
 	// mbik_solve_checked: per-skeleton flag, 1 when any bone's solved basis was non-finite and
 	// was written as the identity rotation (ik_bone_3d.cpp:174-176); null otherwise.
 	unsigned char *nonfinite = nullptr;
@@ -94,6 +99,7 @@ struct DevPlan {
 	// other state at Sg + s * state_stride (one skeleton's LDS layout after its locals)
 	float *Lg = nullptr, *Sg = nullptr;
 	int state_stride = 0;
+	uint32_t lg_bytes = 0, sg_bytes = 0; // their sizes (< 4 GiB: buffer-resource addressing)
 };
 
 // ------------------------------------------------------------------------------------
@@ -115,20 +121,91 @@ __device__ __forceinline__ void st_x(float *p, const X3 &t) {
 	*reinterpret_cast<float4 *>(p + 4) = make_float4(t.b.r[1].y, t.b.r[1].z, t.b.r[2].x, t.b.r[2].y);
 	*reinterpret_cast<float4 *>(p + 8) = make_float4(t.b.r[2].z, t.o.x, t.o.y, t.o.z);
 }
+// Per-lane pointer into device memory as a buffer resource (the base, in SGPRs, uniform over
+// the launch) plus a 32-bit byte offset (one VGPR): the state of placements 1 and 2 is
+// addressed this way instead of by 64-bit per-lane addresses (two VGPRs each, and 64-bit
+// arithmetic per access), which is what pushed the two-waves-per-SIMD build into scratch.
+// Out-of-range offsets read 0 and drop stores instead of faulting (the resource carries the
+// allocation's size).  The host keeps every such area below 4 GiB (ensure_schedule).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void *base, uint32_t bytes) {
+	return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, (int)bytes, 0x00020000);
+}
+template <class T>
+struct BRef {
+	__amdgpu_buffer_rsrc_t r;
+	uint32_t o;
+	__device__ __forceinline__ operator T() const {
+		static_assert(sizeof(T) == 4 || sizeof(T) == 8, "32- or 64-bit elements");
+		if constexpr (sizeof(T) == 4) return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, o, 0, 0));
+		else return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, o, 0, 0));
+	}
+	__device__ __forceinline__ const BRef &operator=(T v) const {
+		if constexpr (sizeof(T) == 4) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, o, 0, 0);
+		else {
+			typedef unsigned int U2 __attribute__((ext_vector_type(2)));
+			__builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(U2, v), r, o, 0, 0);
+		}
+		return *this;
+	}
+};
+template <class T>
+struct BPtr {
+	__amdgpu_buffer_rsrc_t r;
+	uint32_t o;
+	__device__ __forceinline__ BPtr operator+(int i) const { return BPtr{r, o + (uint32_t)(i * (int)sizeof(T))}; }
+	__device__ __forceinline__ BPtr &operator+=(int i) {
+		o += (uint32_t)(i * (int)sizeof(T));
+		return *this;
+	}
+	__device__ __forceinline__ BRef<T> operator[](int i) const { return BRef<T>{r, o + (uint32_t)(i * (int)sizeof(T))}; }
+};
+// The same element type change for raw and buffer pointers (the staged headings' fp64
+// exchange slots, the int flags after the float state).
+template <class T, class U>
+__device__ __forceinline__ T *rebind(U *p) { return reinterpret_cast<T *>(p); }
+template <class T, class U>
+__device__ __forceinline__ BPtr<T> rebind(BPtr<U> p) { return BPtr<T>{p.r, p.o}; }
+// float4 quads through either kind of pointer
+__device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
+__device__ __forceinline__ void st4(float *p, float4 v) { *reinterpret_cast<float4 *>(p) = v; }
+// (element-wise: a 128-bit intrinsic's vector result made the compiler rebuild transforms
+// through scratch; the backend merges the four dword accesses into one dwordx4 again)
+__device__ __forceinline__ float4 ld4(BPtr<float> p) { return make_float4(p[0], p[1], p[2], p[3]); }
+__device__ __forceinline__ void st4(BPtr<float> p, float4 v) {
+	p[0] = v.x;
+	p[1] = v.y;
+	p[2] = v.z;
+	p[3] = v.w;
+}
+__device__ __forceinline__ X3 ld_x(BPtr<float> p) {
+	const float4 a = ld4(p), b = ld4(p + 4), c = ld4(p + 8);
+	X3 t;
+	t.b.r[0] = v3(a.x, a.y, a.z);
+	t.b.r[1] = v3(a.w, b.x, b.y);
+	t.b.r[2] = v3(b.z, b.w, c.x);
+	t.o = v3(c.y, c.z, c.w);
+	return t;
+}
+__device__ __forceinline__ void st_x(BPtr<float> p, const X3 &t) {
+	st4(p, make_float4(t.b.r[0].x, t.b.r[0].y, t.b.r[0].z, t.b.r[1].x));
+	st4(p + 4, make_float4(t.b.r[1].y, t.b.r[1].z, t.b.r[2].x, t.b.r[2].y));
+	st4(p + 8, make_float4(t.b.r[2].z, t.o.x, t.o.y, t.o.z));
+}
+
 // A skeleton's bone locals: transform i's three float4 quads at p + BS*i + QS*{0,1,2}.
 // LocContig (BS 12, QS 4) is one skeleton's [B][12] block (LDS, or the whole state in device
 // memory); LocTiled interleaves the quads of kLocTile consecutive skeletons,
 // [N/kLocTile][B][3][kLocTile][4], so the lanes of one role in a wave (consecutive skeletons,
 // same bone) read whole cache lines.
 constexpr int kLocTile = 16;
-template <int BS, int QS>
+template <int BS, int QS, class PT>
 struct LocV {
-	float *p;
+	PT p;
 	__device__ __forceinline__ X3 ld(int i) const {
-		const float *q = p + BS * i;
-		const float4 a = *reinterpret_cast<const float4 *>(q);
-		const float4 b = *reinterpret_cast<const float4 *>(q + QS);
-		const float4 c = *reinterpret_cast<const float4 *>(q + 2 * QS);
+		const auto q = p + BS * i;
+		const float4 a = ld4(q);
+		const float4 b = ld4(q + QS);
+		const float4 c = ld4(q + 2 * QS);
 		X3 t;
 		t.b.r[0] = v3(a.x, a.y, a.z);
 		t.b.r[1] = v3(a.w, b.x, b.y);
@@ -137,14 +214,15 @@ struct LocV {
 		return t;
 	}
 	__device__ __forceinline__ void st(int i, const X3 &t) const {
-		float *q = p + BS * i;
-		*reinterpret_cast<float4 *>(q) = make_float4(t.b.r[0].x, t.b.r[0].y, t.b.r[0].z, t.b.r[1].x);
-		*reinterpret_cast<float4 *>(q + QS) = make_float4(t.b.r[1].y, t.b.r[1].z, t.b.r[2].x, t.b.r[2].y);
-		*reinterpret_cast<float4 *>(q + 2 * QS) = make_float4(t.b.r[2].z, t.o.x, t.o.y, t.o.z);
+		const auto q = p + BS * i;
+		st4(q, make_float4(t.b.r[0].x, t.b.r[0].y, t.b.r[0].z, t.b.r[1].x));
+		st4(q + QS, make_float4(t.b.r[1].y, t.b.r[1].z, t.b.r[2].x, t.b.r[2].y));
+		st4(q + 2 * QS, make_float4(t.b.r[2].z, t.o.x, t.o.y, t.o.z));
 	}
 };
-using LocContig = LocV<12, 4>;
-using LocTiled = LocV<12 * kLocTile, 4 * kLocTile>;
+using LocContig = LocV<12, 4, float *>;
+template <class PT>
+using LocTiled = LocV<12 * kLocTile, 4 * kLocTile, PT>;
 // SoA per-skeleton tables: element (item, field) of skeleton s.
 #ifdef MBIK_ABLATE_SOA
 #define MBIK_SOA_S(s) ((s) & 15) // timing experiment only: a hot 16-skeleton working set
@@ -153,18 +231,30 @@ using LocTiled = LocV<12 * kLocTile, 4 * kLocTile>;
 #else
 #define MBIK_SOA_S(s) (s)
 #endif
-__device__ __forceinline__ float soa(const float *a, int item, int fields, int f, int N, size_t s) {
-	return a[((size_t)item * fields + f) * N + MBIK_SOA_S(s)];
+constexpr int kRowTile = 16;
+template <bool TL>
+__device__ __forceinline__ size_t row_at(const DevPlan &t, int item, int fields, int f, size_t s) {
+	if constexpr (TL)
+		return (size_t)item * fields * t.row_n + (s / kRowTile) * (size_t)(fields * kRowTile) + (size_t)f * kRowTile + s % kRowTile;
+	else
+		return ((size_t)item * fields + f) * t.N + MBIK_SOA_S(s);
 }
-__device__ __forceinline__ double soad(const double *a, int item, int fields, int f, int N, size_t s) {
-	return a[((size_t)item * fields + f) * N + MBIK_SOA_S(s)];
+// TL: the tiled copy (placement-2 launches); the default is the plan's own layout
+template <bool TL = false>
+__device__ __forceinline__ float soa(const DevPlan &t, const float *a, int item, int fields, int f, size_t s) {
+	return a[row_at<TL>(t, item, fields, f, s)];
 }
-__device__ __forceinline__ B3 ld_soa_basis(const float *a, int item, int fields, int f0, int N, size_t s) {
+template <bool TL = false>
+__device__ __forceinline__ double soad(const DevPlan &t, const double *a, int item, int fields, int f, size_t s) {
+	return a[row_at<TL>(t, item, fields, f, s)];
+}
+template <bool TL = false>
+__device__ __forceinline__ B3 ld_soa_basis(const DevPlan &t, const float *a, int item, int fields, int f0, size_t s) {
 	B3 b;
 #pragma unroll
 	for (int i = 0; i < 3; i++)
-		b.r[i] = v3(soa(a, item, fields, f0 + 3 * i, N, s), soa(a, item, fields, f0 + 3 * i + 1, N, s),
-				soa(a, item, fields, f0 + 3 * i + 2, N, s));
+		b.r[i] = v3(soa<TL>(t, a, item, fields, f0 + 3 * i, s), soa<TL>(t, a, item, fields, f0 + 3 * i + 1, s),
+				soa<TL>(t, a, item, fields, f0 + 3 * i + 2, s));
 	return b;
 }
 
@@ -302,13 +392,15 @@ struct EffPre {
 	float pr[3];
 	double hws[7];
 };
-__device__ __forceinline__ void load_eff(const DevPlan &t, int e, const float *TG, size_t s, const double *hw, EffPre &p,
+template <class FP>
+__device__ __forceinline__ void load_eff(const DevPlan &t, int e, const FP TG, size_t s, const double *hw, EffPre &p,
 		const B3 *Db = nullptr) {
+	constexpr bool TL = std::is_same_v<FP, BPtr<float>>; // placement 2: the tiled table copy
 	p.e = e;
 	p.off = t.eff_path_off[e];
 	p.de = t.eff_path_off[e + 1] - p.off - 1;
 	p.T = ld_x(TG + 12 * e);
-	p.Db = Db ? *Db : ld_soa_basis(t.D, t.eff_bone[e], 9, 0, t.N, s);
+	p.Db = Db ? *Db : ld_soa_basis<TL>(t, t.D, t.eff_bone[e], 9, 0, s);
 	p.hws[0] = hw[0];
 	int k = 1;
 #pragma unroll
@@ -324,29 +416,60 @@ __device__ __forceinline__ void heading_terms(const EffPre &p, const X3 &E, V3 o
 // oe_mode (stabilization, ik_bone_segment_3d.cpp:135-176): 0 plain; 1 also record the target
 // headings' origin in OE; 2 take that origin from OE (target headings are built once per
 // bone-step, before the retry loop, while tip headings are rebuilt on every pass).
-template <class LV>
 // d0: the path index of the solved bone's first descendant (its depth + 1, step record).
+// FP / IP: float / int state pointers (raw LDS pointers, or BPtr into device memory).
+// Path-prefix reuse between consecutive effectors of a segment: their paths from the root
+// share the bones above their branch point (HostPlan::seg_eff_lcp), so an effector's walk
+// starts from the previous walk's product at the last shared depth instead of from the solved
+// bone.  The products and their order are those of separate walks -- bit for bit the same
+// effector globals -- as the reference's IKNode3D caches compute a shared ancestor's global
+// once (ik_node_3d.cpp:33-55).  x is the product down to depth d (d -1: none).
+struct PathCk {
+	X3 x;
+	int d;
+};
+template <class LV, class FP, class IP>
 __device__ __forceinline__ void effector_headings(const DevPlan &t, const EffPre &p, int d0, const X3 &Gb, const LV &L,
-		const float *ST, const int *SF, Headings &H, float *OE = nullptr, int oe_mode = 0) {
+		const FP ST, const IP SF, Headings &H, const FP OE, int oe_mode = 0, PathCk *pc = nullptr, const int *lcp = nullptr) {
 	const int e = p.e;
 	X3 E;
 	if (SF[e]) {
 		E = ld_x(ST + 12 * e); // stale bone-direction cache (ik_node_3d.cpp:56-67 never propagates)
+		if (pc) pc->d = -1;
 	} else {
 		X3 X = Gb;
 		const int off = p.off;
 		const int de = p.de;
-		int d = d0;
-		if (d <= de) {
-			// software-pipelined: the next path bone's local pose loads during this product
-			X3 Ln = L.ld(t.eff_path[off + d]);
-			for (; d < de; d++) {
+		// X *= L(path[d]) for d = a..b, software-pipelined: the next path bone's local pose
+		// loads during the current product
+		auto walk = [&](int a, int b) {
+			if (a > b) return;
+			X3 Ln = L.ld(t.eff_path[off + a]);
+			for (int d = a; d < b; d++) {
 				const X3 Lc = Ln;
 				Ln = L.ld(t.eff_path[off + d + 1]);
 				X = X * Lc;
 			}
 			X = X * Ln;
+		};
+		int d = d0;
+		if (pc) {
+			// lcp[0]: depths shared with the previous effector; lcp[1]: with the next one
+			const int l = lcp[0];
+			if (pc->d >= d0 && pc->d == l - 1) {
+				X = pc->x;
+				d = l;
+			}
+			pc->d = -1;
+			const int cpd = lcp[1] - 1;
+			if (cpd >= d && cpd <= de) {
+				walk(d, cpd);
+				pc->x = X;
+				pc->d = cpd;
+				d = cpd + 1;
+			}
 		}
+		walk(d, de);
 		E.b = X.b * p.Db;
 		E.o = X.o;
 	}
@@ -358,13 +481,13 @@ __device__ __forceinline__ void effector_headings(const DevPlan &t, const EffPre
 	}
 	heading_terms(p, E, oe, Gb.o, H);
 }
-template <class LV>
+template <class LV, class FP, class IP>
 __device__ __forceinline__ void effector_headings(const DevPlan &t, int e, int d0, const X3 &Gb, const LV &L,
-		const float *TG, const float *ST, const int *SF, size_t s, const double *hw, Headings &H, float *OE = nullptr,
-		int oe_mode = 0, const B3 *Db = nullptr) {
+		const FP TG, const FP ST, const IP SF, size_t s, const double *hw, Headings &H, const FP OE,
+		int oe_mode = 0, const B3 *Db = nullptr, PathCk *pc = nullptr, const int *lcp = nullptr) {
 	EffPre p;
 	load_eff(t, e, TG, s, hw, p, Db);
-	effector_headings(t, p, d0, Gb, L, ST, SF, H, OE, oe_mode);
+	effector_headings(t, p, d0, Gb, L, ST, SF, H, OE, oe_mode, pc, lcp);
 }
 
 // The heading pairs of effector p.e (ik_effector_3d.cpp:90-149): E = the effector bone's
@@ -454,6 +577,16 @@ __device__ __forceinline__ V3 great_tangent_triangle(V3 c1xc2, V3 a1, V3 a2, V3 
 	return v3(NAN, NAN, NAN);
 }
 
+#ifdef MBIK_NO_PATH_REUSE
+constexpr bool kPathReuse = false; // A/B switch
+#else
+constexpr bool kPathReuse = true;
+#endif
+#ifdef MBIK_PATH_REUSE_2W
+constexpr bool kPathReuse2W = true; // the two-wave build as well (A/B)
+#else
+constexpr bool kPathReuse2W = false;
+#endif
 #ifndef MBIK_STEP_ATTR
 #define MBIK_STEP_ATTR
 #endif
@@ -461,6 +594,7 @@ __device__ __forceinline__ V3 great_tangent_triangle(V3 c1xc2, V3 a1, V3 a2, V3 
 #define MBIK_LIMITS_ATTR
 #endif
 // IKKusudama3D::get_local_point_in_limits (ik_kusudama_3d.cpp:273-332)
+template <bool TL = false>
 __device__ MBIK_LIMITS_ATTR V3 local_point_in_limits(const DevPlan &t, int slot, size_t s, V3 in_point, double &in_bounds) {
 	const int nc = t.cons_ncones[slot];
 	V3 point = normalized(in_point);
@@ -470,9 +604,9 @@ __device__ MBIK_LIMITS_ATTR V3 local_point_in_limits(const DevPlan &t, int slot,
 	const V3 npoint = normalized(point); // closest_to_cone's input.normalized(), the same for every cone
 	for (int i = 0; i < nc; i++) {
 		const int o = mbik::CF_CONE0 + mbik::CF_PER_CONE * i;
-		auto f = [&](int k) { return soa(t.CF, slot, t.cf_stride, o + k, t.N, s); };
+		auto f = [&](int k) { return soa<TL>(t, t.CF, slot, t.cf_stride, o + k, s); };
 		V3 ncp = v3(f(mbik::CFC_NCP), f(mbik::CFC_NCP + 1), f(mbik::CFC_NCP + 2));
-		double rcos = soad(t.CD, slot, t.cd_stride, mbik::CD_PER_CONE * i, t.N, s);
+		double rcos = soad<TL>(t, t.CD, slot, t.cd_stride, mbik::CD_PER_CONE * i, s);
 		V3 c = closest_to_cone(ncp, f(mbik::CFC_SR), f(mbik::CFC_CR), rcos, npoint, in_bounds);
 		if (is_nan3(c)) {
 			in_bounds = 1;
@@ -487,9 +621,9 @@ __device__ MBIK_LIMITS_ATTR V3 local_point_in_limits(const DevPlan &t, int slot,
 	if (in_bounds == -1) {
 		for (int i = 0; i + 1 < nc; i++) {
 			const int o = mbik::CF_CONE0 + mbik::CF_PER_CONE * i;
-			auto f = [&](int k) { return soa(t.CF, slot, t.cf_stride, k, t.N, s); };
+			auto f = [&](int k) { return soa<TL>(t, t.CF, slot, t.cf_stride, k, s); };
 			auto f3 = [&](int k) { return v3(f(o + k), f(o + k + 1), f(o + k + 2)); };
-			double trcos = soad(t.CD, slot, t.cd_stride, mbik::CD_PER_CONE * i + 1, t.N, s);
+			double trcos = soad<TL>(t, t.CD, slot, t.cd_stride, mbik::CD_PER_CONE * i + 1, s);
 			V3 c = great_tangent_triangle(f3(mbik::CFC_C1XC2), f3(mbik::CFC_A1), f3(mbik::CFC_A2), f3(mbik::CFC_B1),
 					f3(mbik::CFC_B2), f3(mbik::CFC_T1), f3(mbik::CFC_T2), f(o + mbik::CFC_ST), f(o + mbik::CFC_CT), trcos, point);
 			if (isnan(c.x)) continue;
@@ -531,7 +665,8 @@ __device__ __forceinline__ void wave_sync_lds() {
 // Staged-heading record (multi-lane segments): the 11 QCP::inner_product terms of one heading
 // pair, as floats -- wc1_a * c2_b (a, b = x, y, z), dot(wc1, c1), dot(c2, c2).
 constexpr int HS_REC = 12;
-__device__ __forceinline__ void qcp_terms(const V3 wc1, const V3 c1, const V3 c2, float *r) {
+template <class FP>
+__device__ __forceinline__ void qcp_terms(const V3 wc1, const V3 c1, const V3 c2, const FP r) {
 	r[0] = wc1.x * c2.x; r[1] = wc1.x * c2.y; r[2] = wc1.x * c2.z;
 	r[3] = wc1.y * c2.x; r[4] = wc1.y * c2.y; r[5] = wc1.y * c2.z;
 	r[6] = wc1.z * c2.x; r[7] = wc1.z * c2.y; r[8] = wc1.z * c2.z;
@@ -540,9 +675,11 @@ __device__ __forceinline__ void qcp_terms(const V3 wc1, const V3 c1, const V3 c2
 }
 // STAB: the plan has stabilization passes (a separate instantiation keeps the retry loop and
 // its LDS staging out of the default kernel).
-template <bool STAB, class LV>
-__device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j, int m, size_t s, const LV &L, const float *G, const float *TG,
-		float *ST, int *SF, float *HS, float *OE, float *MS, double &prev_dev, const EffPre &pre, bool hoist, bool dbh MBIK_PROF_PARAM) {
+// PR: reuse effector path prefixes (PathCk) in multi-effector segments solved from registers.
+template <bool STAB, bool PR, class LV, class FP, class IP>
+__device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j, int m, size_t s, const LV &L, const FP G, const FP TG,
+		const FP ST, const IP SF, const FP HS, const FP OE, const FP MS, double &prev_dev, const EffPre &pre, bool hoist, bool dbh MBIK_PROF_PARAM) {
+	constexpr bool TL = std::is_same_v<FP, BPtr<float>>; // placement 2: the tiled table copy
 	MBIK_PROF_T(pt0);
 #ifdef MBIK_PROF
 	uint64_t pt1 = pt0, pt3 = pt0;
@@ -609,9 +746,12 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 		V3 mc = v3(0, 0, 0), tc = v3(0, 0, 0);
 		if (translate) {
 			double wsum = 0;
+			PathCk pc;
+			pc.d = -1;
 			for (int i = e0; i < e1; i++) {
 				if (hoist) effector_headings(t, pre, d0, Gb, L, ST, SF, H, OE, oe_mode);
-				else effector_headings(t, t.seg_effs[i], d0, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, oe_mode, dbh ? &pre.Db : nullptr);
+				else effector_headings(t, t.seg_effs[i], d0, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, oe_mode,
+						dbh ? &pre.Db : nullptr, PR ? &pc : nullptr, t.seg_eff_lcp + i);
 #pragma unroll
 				for (int h = 0; h < 7; h++) {
 					if (H.mask & (1 << h)) {
@@ -629,10 +769,13 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 		}
 		QSums S = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 		const V3 nmc = mc * -1.0f, ntc = tc * -1.0f;
+		PathCk pc;
+		pc.d = -1;
 		for (int i = e0; i < e1; i++) {
 			MBIK_PROF_T(ph1);
 			if (hoist) effector_headings(t, pre, d0, Gb, L, ST, SF, H, OE, oe_mode);
-			else effector_headings(t, t.seg_effs[i], d0, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, oe_mode, dbh ? &pre.Db : nullptr);
+			else effector_headings(t, t.seg_effs[i], d0, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, oe_mode,
+					dbh ? &pre.Db : nullptr, PR ? &pc : nullptr, t.seg_eff_lcp + i);
 			MBIK_PROF_T(ph2);
 			MBIK_PROF_ADD(9, ph1, ph2);
 #pragma unroll
@@ -674,14 +817,14 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 		//      go through LDS and the lanes turn their records into centred terms;
 		//   3. lane j takes the inner-product sums q = j, j+m, ... < 11, exchanged through LDS.
 		// Each sum is accumulated in exactly the reference's order and rounding.
-		float *hsg = HS + t.seg_hbase[seg];
-		double *ex = reinterpret_cast<double *>(hsg + HS_REC * nh);
+		const auto hsg = HS + t.seg_hbase[seg];
+		const auto ex = rebind<double>(hsg + HS_REC * nh);
 		for (int i = e0 + j; i < e1; i += m) {
 			MBIK_PROF_T(ph1);
 			effector_headings(t, t.seg_effs[i], d0, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, oe_mode);
 			MBIK_PROF_T(ph2);
 			MBIK_PROF_ADD(9, ph1, ph2);
-			float *r = hsg + HS_REC * t.seg_eff_hoff[i];
+			auto r = hsg + HS_REC * t.seg_eff_hoff[i];
 #pragma unroll
 			for (int h = 0; h < 7; h++) {
 				if (H.mask & (1 << h)) {
@@ -706,7 +849,7 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 			const int p0 = q0 < 6 ? o0 : 0, p1 = q1 < 6 ? o1 : 0;
 			int c = 0;
 			for (; c + 4 <= nh; c += 4) { // 4 headings per LDS round trip
-				const float *r = hsg + HS_REC * c;
+				const auto r = hsg + HS_REC * c;
 				float x0[4], x1[4];
 				double w[4];
 #pragma unroll
@@ -724,7 +867,7 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 				}
 			}
 			for (; c < nh; c++) {
-				const float *r = hsg + HS_REC * c;
+				const auto r = hsg + HS_REC * c;
 				const double w = hw[c];
 				const float wf = (float)w;
 				fa0 = fa0 + r[p0] * wf;
@@ -751,7 +894,7 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 			const V3 nmc = mc * -1.0f, ntc = tc * -1.0f;
 			wave_sync_lds();
 			for (int c = j; c < nh; c += m) {
-				float *r = hsg + HS_REC * c;
+				const auto r = hsg + HS_REC * c;
 				const V3 c1 = v3(r[0], r[1], r[2]) + ntc;
 				const V3 c2 = v3(r[3], r[4], r[5]) + nmc;
 				qcp_terms(c1 * (float)hw[c], c1, c2, r);
@@ -765,7 +908,7 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 			const int i0 = q0 < 11 ? q0 : 0, i1 = q1 < 11 ? q1 : 0, i2 = q2 < 11 ? q2 : 0;
 			int c = 0;
 			for (; c + 4 <= nh; c += 4) { // 4 headings per LDS round trip
-				const float *r = hsg + HS_REC * c;
+				const auto r = hsg + HS_REC * c;
 				float x0[4], x1[4], x2[4];
 				double w[4];
 #pragma unroll
@@ -783,7 +926,7 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 				}
 			}
 			for (; c < nh; c++) {
-				const float *r = hsg + HS_REC * c;
+				const auto r = hsg + HS_REC * c;
 				const double w0 = hw[c];
 				const float x0 = r[q0], x1 = r[q1 < 11 ? q1 : 0], x2 = r[q2 < 11 ? q2 : 0];
 				a0 += q0 == 10 ? w0 * (double)x0 : (double)x0;
@@ -798,7 +941,7 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 				double b0 = 0.0, b1 = 0.0, b2 = 0.0;
 				const int p0 = j + 6, p1 = j + 8, p2 = j + 10;
 				for (c = 0; c < nh; c++) {
-					const float *r = hsg + HS_REC * c;
+					const auto r = hsg + HS_REC * c;
 					const double w0 = hw[c];
 					b0 += (double)r[p0];
 					b1 += (double)r[p1];
@@ -881,13 +1024,13 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 		X3 Gs = P * Lb;
 		GsB = Gs.b;
 		gs_ok = true;
-		Gbd_stale.b = Gs.b * ld_soa_basis(t.D, b, 9, 0, t.N, s);
+		Gbd_stale.b = Gs.b * ld_soa_basis<TL>(t, t.D, b, 9, 0, s);
 		Gbd_stale.o = Gs.o;
 		X3 Gco = {P.b, xform(P, Lb.o)}; // constraint_orientation: (I, pose local origin) under the parent
 		V3 bdx = xform(Gbd_stale, v3(0.0f, 1.0f, 0.0f));
 		V3 tip = xform(X3{Pinv, xform(Pinv, -Gco.o)}, bdx); // Gco.basis == P.basis
 		double in_bounds = 1.0;
-		V3 inl = local_point_in_limits(t, slot, s, tip, in_bounds);
+		V3 inl = local_point_in_limits<TL>(t, slot, s, tip, in_bounds);
 		if (in_bounds < 0) {
 			V3 p2 = xform(Gco, inl);
 			Q rect = arc(bdx - Gco.o, p2 - Gco.o);
@@ -905,10 +1048,10 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 	if (flags & mbik::BF_AXIAL) {
 #endif
 		const int cs = t.cf_stride;
-		Q tcr = q4(soa(t.CF, slot, cs, mbik::CF_TWIST_Q, t.N, s), soa(t.CF, slot, cs, mbik::CF_TWIST_Q + 1, t.N, s),
-				soa(t.CF, slot, cs, mbik::CF_TWIST_Q + 2, t.N, s), soa(t.CF, slot, cs, mbik::CF_TWIST_Q + 3, t.N, s));
-		float half_cos = soa(t.CF, slot, cs, mbik::CF_TWIST_COS, t.N, s);
-		B3 Tb = ld_soa_basis(t.CF, slot, cs, mbik::CF_TWIST_T, t.N, s);
+		Q tcr = q4(soa<TL>(t, t.CF, slot, cs, mbik::CF_TWIST_Q, s), soa<TL>(t, t.CF, slot, cs, mbik::CF_TWIST_Q + 1, s),
+				soa<TL>(t, t.CF, slot, cs, mbik::CF_TWIST_Q + 2, s), soa<TL>(t, t.CF, slot, cs, mbik::CF_TWIST_Q + 3, s));
+		float half_cos = soa<TL>(t, t.CF, slot, cs, mbik::CF_TWIST_COS, s);
+		B3 Tb = ld_soa_basis<TL>(t, t.CF, slot, cs, mbik::CF_TWIST_T, s);
 		B3 Gct = P.b * Tb;
 		X3 Gs;
 		if (gs_ok && !swung) Gs.b = GsB;
@@ -989,8 +1132,8 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 }
 
 // Iteration-start globals of one segment, root -> tip (IKNode3D::get_global_transform).
-template <class LV>
-__device__ void global_pass(const DevPlan &t, int seg, const LV &L, float *G) {
+template <class LV, class FP>
+__device__ void global_pass(const DevPlan &t, int seg, const LV &L, const FP G) {
 	X3 Gprev = xid();
 	for (int k = t.seg_bone_off[seg + 1] - 1; k >= t.seg_bone_off[seg]; k--) {
 		const int b = t.seg_bones[k];
@@ -1069,24 +1212,32 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 	const int B = t.B, P = t.P, K = t.K;
 	// PL (HostPlan::state_hbm): 0 the state in LDS; 1 the locals in device memory (L2-resident
 	// during the launch), the rest in LDS; 2 all of it in device memory
-	using LV = std::conditional_t<PL >= 1, LocTiled, LocContig>;
+	// FP / IP: the float / int state pointers: LDS, or for PL 2 BPtr into device memory.  (PL 1
+	// keeps 64-bit pointers to its locals: in its two-wave build, C3's pick, the buffer form
+	// spilled more, not less.)
+	using FP = std::conditional_t<PL == 2, BPtr<float>, float *>;
+	using IP = std::conditional_t<PL == 2, BPtr<int>, int *>;
+	using LV = std::conditional_t<PL >= 1, LocTiled<FP>, LocContig>;
 	LV L;
-	float *G;
-	if constexpr (PL >= 1) L.p = t.Lg + (s / kLocTile) * (size_t)(12 * kLocTile) * B + (s % kLocTile) * 4;
+	FP G;
+	const size_t loc0 = (s / kLocTile) * (size_t)(12 * kLocTile) * B + (s % kLocTile) * 4;
+	if constexpr (PL == 2) L.p = BPtr<float>{buf_rsrc(t.Lg, t.lg_bytes), (uint32_t)(loc0 * sizeof(float))};
+	else if constexpr (PL == 1) L.p = t.Lg + loc0;
 	if constexpr (PL == 2) {
-		G = t.Sg + s * (size_t)t.state_stride;
+		G = BPtr<float>{buf_rsrc(t.Sg, t.sg_bytes), (uint32_t)(s * (size_t)t.state_stride * sizeof(float))};
 	} else if constexpr (PL == 1) {
 		G = lds + (size_t)g * t.lds_stride;
 	} else {
 		L.p = lds + (size_t)g * t.lds_stride;
 		G = L.p + 12 * B;
 	}
-	float *TG = G + 12 * t.n_gck;
-	float *ST = TG + 12 * P;
-	float *HS = ST + 12 * P;                        // staged headings (t.seg_hbase), 16-B aligned
-	int *SF = reinterpret_cast<int *>(HS + t.hs_floats);
-	float *OE = reinterpret_cast<float *>(SF + P);  // stabilization only: 3 per pin
-	float *MS = OE + 3 * P;                        // stabilization only: 7 per pin
+	const FP TG = G + 12 * t.n_gck;
+	const FP ST = TG + 12 * P;
+	const FP HS = ST + 12 * P;                        // staged headings (t.seg_hbase), 16-B aligned
+	const IP SF = rebind<int>(HS + t.hs_floats);
+	constexpr bool TL = PL == 2; // placement 2 reads the tiled table copy
+	const FP OE = rebind<float>(SF + P);              // stabilization only: 3 per pin
+	const FP MS = OE + 3 * P;                        // stabilization only: 7 per pin
 	if (valid) {
 		for (int b = role; b < B; b += K)
 			if (t.bone_flags[b] & mbik::BF_IN_LIST) L.st(b, pose_to_xform(pose_in + ((size_t)local * B + b) * 10));
@@ -1123,9 +1274,9 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 				// The two-wave build hoists only the effector's bone-direction basis (its nine
 				// device-memory loads per bone-step; C3 4.15 -> 4.08 ms).
 				const bool dbh = !HOIST && !STAB && t.seg_eff_off[seg + 1] - e0 == 1;
-				if (dbh) pre.Db = ld_soa_basis(t.D, t.eff_bone[t.seg_effs[e0]], 9, 0, t.N, s);
+				if (dbh) pre.Db = ld_soa_basis<TL>(t, t.D, t.eff_bone[t.seg_effs[e0]], 9, 0, s);
 				for (int k = t.seg_bone_off[seg]; k < t.seg_bone_off[seg + 1]; k++)
-					bone_step<STAB>(t, seg, k, task.y, task.z, s, L, G, TG, ST, SF, HS, OE, MS, prev_dev, pre, hoist, dbh MBIK_PROF_ARG);
+					bone_step<STAB, kPathReuse && (HOIST || PL == 2 || kPathReuse2W)>(t, seg, k, task.y, task.z, s, L, G, TG, ST, SF, HS, OE, MS, prev_dev, pre, hoist, dbh MBIK_PROF_ARG);
 			}
 			__syncthreads();
 		}
@@ -1250,6 +1401,18 @@ struct TopoSlice {
 	int32_t *scr_i;
 	double *scr_d;
 };
+// [items*fields][N] -> [items][Npad/kRowTile][fields][kRowTile] (DevPlan::row_at), one element a thread
+template <class T>
+__global__ __launch_bounds__(256) void mbik_tile_rows_kernel(const T *__restrict__ src, T *__restrict__ dst, int items,
+		int fields, int N, int Npad) {
+	const size_t n = (size_t)items * fields * N;
+	for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+		const size_t row = i / N, sk = i % N;
+		const size_t item = row / fields, f = row % fields;
+		dst[item * fields * Npad + (sk / kRowTile) * fields * kRowTile + f * kRowTile + sk % kRowTile] = src[i];
+	}
+}
+
 __global__ __launch_bounds__(64) void mbik_topology_kernel(const TopoSlice *__restrict__ slices, int n) {
 	const int i = blockIdx.x * blockDim.x + threadIdx.x;
 	if (i >= n) return;
@@ -1300,6 +1463,11 @@ struct mbik_plan {
 	int32_t src_max_cones = 1;
 	mbik_config src_cfg{};
 	bool setup_on_device = false; // mbik_plan_create_device: the setup pose given to finish_plan is a device buffer
+	// skeleton-tiled copies of D / CF / CD for launches with the whole state in device memory
+	// (DevPlan::row_at); rebuilt when the tables changed since (tables_version)
+	float *d_Dt = nullptr, *d_CFt = nullptr;
+	double *d_CDt = nullptr;
+	int tables_version = 1, tiled_version = 0;
 };
 
 namespace {
@@ -1396,6 +1564,8 @@ int blocks_per_cu(void *ctx, int64_t lds_bytes) {
 // cheap and its state lives in HBM, so the chip's VALU issue (many narrow waves), not one
 // skeleton's chain, bounds it beyond that (C2 / C3 / C5: DESIGN.md §1, profiles/r01_cmode_lanes_sweep.jsonl).
 constexpr int kCmodeLanes = 4;
+// device-memory state areas are addressed through buffer resources (32-bit byte offsets)
+constexpr size_t kMaxBufBytes = 0xFFFFFFF0u;
 
 int ensure_schedule(mbik_plan *p, int64_t nlaunch) {
 	mbik::HostPlan &h = p->host;
@@ -1411,6 +1581,7 @@ int ensure_schedule(mbik_plan *p, int64_t nlaunch) {
 		p->allocs.push_back(p->d_locals);
 		p->device_bytes += (int64_t)bytes;
 		p->dev.Lg = p->d_locals;
+		p->dev.lg_bytes = (uint32_t)std::min<size_t>(bytes, 0xFFFFFFFFu); // (placement 2 refuses > kMaxBufBytes)
 	}
 	mbik::build_schedule(h, lanes, nlaunch, p->spw_override, p->interval_override, blocks_per_cu, p, p->cu_count);
 	if (lanes == 0 && h.constraint_mode && h.K > kCmodeLanes)
@@ -1420,6 +1591,8 @@ int ensure_schedule(mbik_plan *p, int64_t nlaunch) {
 		// (the locals live in the tiled area, d_locals)
 		const int stride = (mbik::state_floats_per_skeleton(h) - 12 * h.B + 3) & ~3;
 		const size_t need = (size_t)h.N * stride;
+		if (need * sizeof(float) > kMaxBufBytes || p->dev.lg_bytes > kMaxBufBytes)
+			return fail(MBIK_EUNSUPPORTED, "solve state in device memory needs < 4 GiB per area (fewer skeletons per plan)");
 		if (need > p->d_state_floats) {
 			void *a = nullptr;
 			if (hipMalloc(&a, need * sizeof(float)) != hipSuccess) return fail(MBIK_ENOMEM, "hipMalloc state");
@@ -1434,6 +1607,7 @@ int ensure_schedule(mbik_plan *p, int64_t nlaunch) {
 			p->device_bytes += (int64_t)(need * sizeof(float));
 		}
 		p->dev.Sg = p->d_state;
+		p->dev.sg_bytes = (uint32_t)(p->d_state_floats * sizeof(float));
 		p->dev.state_stride = stride;
 	}
 	if (p->sched_K == h.K && p->sched_c == h.g_interval && p->sched_staging == (int)h.staging &&
@@ -1520,6 +1694,50 @@ int cmode_create(mbik_plan *p, const float *setup_pose, const void *saved) {
 	return rc;
 }
 
+// The skeleton-tiled copies of the plan's D / CF / CD (DevPlan::row_at) for launches with the
+// whole state in device memory, (re)built on the launch stream when the tables changed.
+int ensure_tiled_rows(mbik_plan *p, hipStream_t stream) {
+	if (p->tiled_version == p->tables_version && p->d_Dt) return MBIK_OK;
+	const mbik::HostPlan &h = p->host;
+	const int Npad = (h.N + kRowTile - 1) / kRowTile * kRowTile;
+	const size_t nD = (size_t)h.B * 9 * Npad, nCF = (size_t)h.NC * h.cf_stride() * Npad, nCD = (size_t)h.NC * h.cd_stride() * Npad;
+	if (!p->d_Dt) {
+		void *a = nullptr, *b = nullptr, *c = nullptr;
+		if (hipMalloc(&a, std::max<size_t>(nD, 1) * sizeof(float)) != hipSuccess ||
+				hipMalloc(&b, std::max<size_t>(nCF, 1) * sizeof(float)) != hipSuccess ||
+				hipMalloc(&c, std::max<size_t>(nCD, 1) * sizeof(double)) != hipSuccess) {
+			if (a) (void)hipFree(a);
+			if (b) (void)hipFree(b);
+			if (c) (void)hipFree(c);
+			return fail(MBIK_ENOMEM, "hipMalloc tiled setup tables");
+		}
+		// padding skeletons read zeros
+		if (hipMemsetAsync(a, 0, std::max<size_t>(nD, 1) * sizeof(float), stream) != hipSuccess ||
+				hipMemsetAsync(b, 0, std::max<size_t>(nCF, 1) * sizeof(float), stream) != hipSuccess ||
+				hipMemsetAsync(c, 0, std::max<size_t>(nCD, 1) * sizeof(double), stream) != hipSuccess)
+			return fail(MBIK_EHIP, "hipMemsetAsync tiled setup tables");
+		p->d_Dt = static_cast<float *>(a);
+		p->d_CFt = static_cast<float *>(b);
+		p->d_CDt = static_cast<double *>(c);
+		p->allocs.push_back(a);
+		p->allocs.push_back(b);
+		p->allocs.push_back(c);
+		p->device_bytes += (int64_t)((nD + nCF) * sizeof(float) + nCD * sizeof(double));
+	}
+	auto grid = [](size_t n) { return dim3((unsigned)std::min<size_t>((n + 255) / 256, 65536)); };
+	if (nD) hipLaunchKernelGGL(mbik_tile_rows_kernel<float>, grid(nD), dim3(256), 0, stream, p->dev.D, p->d_Dt, h.B, 9, h.N, Npad);
+	if (nCF)
+		hipLaunchKernelGGL(mbik_tile_rows_kernel<float>, grid(nCF), dim3(256), 0, stream, p->dev.CF, p->d_CFt, h.NC,
+				h.cf_stride(), h.N, Npad);
+	if (nCD)
+		hipLaunchKernelGGL(mbik_tile_rows_kernel<double>, grid(nCD), dim3(256), 0, stream, p->dev.CD, p->d_CDt, h.NC,
+				h.cd_stride(), h.N, Npad);
+	hipError_t e = hipGetLastError();
+	if (e != hipSuccess) return fail(MBIK_EHIP, std::string("tile launch failed: ") + hipGetErrorString(e));
+	p->tiled_version = p->tables_version;
+	return MBIK_OK;
+}
+
 int launch(mbik_plan *p, int first, int count, const float *pose_in, const float *targets, float *pose_out,
 		hipStream_t stream, int iterations, int seg_lo, int seg_hi) {
 	if (first < 0 || count < 0 || (int64_t)first + count > p->host.N) return fail(MBIK_EINVAL, "skeleton range out of plan");
@@ -1559,7 +1777,15 @@ int launch(mbik_plan *p, int first, int count, const float *pose_in, const float
 	if (lds > 160 * 1024) return fail(MBIK_EUNSUPPORTED, "skeleton too large for LDS at this lane count");
 	unsigned blocks = (unsigned)((count + h.spw - 1) / h.spw);
 	auto kern = solve_kernel_for(h);
-	hipLaunchKernelGGL(kern, dim3(blocks), dim3(64), lds, stream, p->dev, first, count, pose_in, targets, pose_out,
+	DevPlan d = p->dev;
+	if (h.state_hbm == 2) {
+		if ((rc = ensure_tiled_rows(p, stream)) != MBIK_OK) return rc;
+		d.D = p->d_Dt;
+		d.CF = p->d_CFt;
+		d.CD = p->d_CDt;
+		d.row_n = (h.N + kRowTile - 1) / kRowTile * kRowTile;
+	}
+	hipLaunchKernelGGL(kern, dim3(blocks), dim3(64), lds, stream, d, first, count, pose_in, targets, pose_out,
 			iterations, seg_lo, seg_hi);
 	hipError_t e = hipGetLastError();
 	if (e != hipSuccess) return fail(MBIK_EHIP, std::string("kernel launch failed: ") + hipGetErrorString(e));
@@ -2246,6 +2472,7 @@ int32_t mbik_plan_rebuild_setup(mbik_plan *p, int32_t first, int32_t count, cons
 	(void)hipFree(scratch);
 	if (e != hipSuccess) return fail(MBIK_EHIP, std::string("setup launch: ") + hipGetErrorString(e));
 	if (es != hipSuccess) return fail(MBIK_EHIP, std::string("setup kernel: ") + hipGetErrorString(es));
+	p->tables_version++;
 	// a rebuilt tree starts with fresh node caches (_bone_list_changed)
 	if (h.constraint_mode) return cmode_reset(p, first, count, setup_pose, st);
 	return MBIK_OK;
@@ -2420,7 +2647,14 @@ int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const flo
 		p->staging_override = stg;
 		p->locals_override = lh;
 		p->waves_override = wv;
-		if ((rc = ensure_schedule(p, count)) != MBIK_OK) break;
+		if ((rc = ensure_schedule(p, count)) != MBIK_OK) {
+			// a placement this batch cannot have (device memory, or the 4 GiB buffer limit) is skipped
+			if (rc == MBIK_ENOMEM || rc == MBIK_EUNSUPPORTED) {
+				rc = MBIK_OK;
+				continue;
+			}
+			break;
+		}
 		const auto key = std::make_tuple(p->host.K, p->host.spw, p->host.g_interval, stg, lh, wv);
 		if (std::find(seen.begin(), seen.end(), key) != seen.end()) continue;
 		seen.push_back(key);

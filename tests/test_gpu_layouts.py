@@ -214,3 +214,29 @@ def test_tuned_full_size_layouts_are_exact(oracle, mbik, cfg, n, pin):
         sub = W.generate(cfg, 6, first=first)
         ref = oracle.Oracle(sub).solve(sub.pose, sub.targets, threads=8)
         assert_parity(got[first:first + 6], ref, f"C{cfg} tuned layout {info} @{first}")
+
+
+@pytest.mark.parametrize("waves", [1, 2])
+def test_state_in_hbm_reads_rebuilt_setup_tables(oracle, mbik, waves):
+    """Placement 2 reads a skeleton-tiled copy of the per-skeleton tables (DevPlan::row_n):
+    after mbik_plan_rebuild_setup the copy is rebuilt, so the solve follows the new rest poses,
+    cones and twist like a plan created from them (bitwise, 19 skeletons: a ragged last tile)."""
+    import torch
+    wl = W.generate(5, 19, first=40)
+    other = W.generate(5, 19, first=900)                     # other rest poses, cones, twist
+    plan = Plan.from_workload(wl)
+    plan.set_locals_placement(2)
+    plan.set_waves_per_simd(waves)
+    first = plan.solve_host(wl.pose, wl.targets)             # builds the tiled copy of wl's tables
+    assert_parity(first, oracle.Oracle(wl).solve(wl.pose, wl.targets, threads=8), "placement 2 before rebuild")
+    dev = torch.device("cuda", 0)
+    sp = torch.from_numpy(other.pose).to(dev)
+    cn = torch.from_numpy(np.ascontiguousarray(other.cones)).to(dev)
+    tw = torch.from_numpy(np.ascontiguousarray(other.twist)).to(dev)
+    plan.rebuild_setup(sp.data_ptr(), cn.data_ptr(), tw.data_ptr(), stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    got = plan.solve_host(wl.pose, wl.targets)
+    fresh = Plan.from_workload(other)
+    want = fresh.solve_host(wl.pose, wl.targets)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+    assert not np.array_equal(got.view(np.uint32), first.view(np.uint32))
