@@ -582,6 +582,16 @@ constexpr bool kPathReuse = false; // A/B switch
 #else
 constexpr bool kPathReuse = true;
 #endif
+#ifdef MBIK_NO_DBH_PL2
+constexpr bool kNoDbhPl2 = true; // A/B switches
+#else
+constexpr bool kNoDbhPl2 = false;
+#endif
+#ifdef MBIK_NO_PR_PL2
+constexpr bool kNoPrPl2 = true;
+#else
+constexpr bool kNoPrPl2 = false;
+#endif
 #ifdef MBIK_PATH_REUSE_2W
 constexpr bool kPathReuse2W = true; // the two-wave build as well (A/B)
 #else
@@ -1273,10 +1283,10 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 				if (hoist) load_eff(t, t.seg_effs[e0], TG, s, t.seg_hw + t.seg_hw_off[seg] + t.seg_eff_hoff[e0], pre);
 				// The two-wave build hoists only the effector's bone-direction basis (its nine
 				// device-memory loads per bone-step; C3 4.15 -> 4.08 ms).
-				const bool dbh = !HOIST && !STAB && t.seg_eff_off[seg + 1] - e0 == 1;
+				const bool dbh = !HOIST && !STAB && !(kNoDbhPl2 && PL == 2) && t.seg_eff_off[seg + 1] - e0 == 1;
 				if (dbh) pre.Db = ld_soa_basis<TL>(t, t.D, t.eff_bone[t.seg_effs[e0]], 9, 0, s);
 				for (int k = t.seg_bone_off[seg]; k < t.seg_bone_off[seg + 1]; k++)
-					bone_step<STAB, kPathReuse && (HOIST || PL == 2 || kPathReuse2W)>(t, seg, k, task.y, task.z, s, L, G, TG, ST, SF, HS, OE, MS, prev_dev, pre, hoist, dbh MBIK_PROF_ARG);
+					bone_step<STAB, kPathReuse && (HOIST || (PL == 2 && !kNoPrPl2) || kPathReuse2W)>(t, seg, k, task.y, task.z, s, L, G, TG, ST, SF, HS, OE, MS, prev_dev, pre, hoist, dbh MBIK_PROF_ARG);
 			}
 			__syncthreads();
 		}
