@@ -582,10 +582,14 @@ constexpr bool kPathReuse = false; // A/B switch
 #else
 constexpr bool kPathReuse = true;
 #endif
-#ifdef MBIK_NO_DBH_PL2
-constexpr bool kNoDbhPl2 = true; // A/B switches
+// The two-wave build used to hold a single-effector segment's bone-direction basis across the
+// segment (round 1: C3 -2 %).  With the state addressing and path sharing of round 2 those nine
+// registers spilled instead (placement 2: 31 spilled registers with them, 22 without), and
+// reading the basis at each step is faster: C3 -1 %, C4 -1.6 %, C5 -3 % (same-box A/B).
+#ifdef MBIK_DBH
+constexpr bool kDbh = true; // A/B switch
 #else
-constexpr bool kNoDbhPl2 = false;
+constexpr bool kDbh = false;
 #endif
 #ifdef MBIK_NO_PR_PL2
 constexpr bool kNoPrPl2 = true;
@@ -1281,9 +1285,9 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 				// push that build past 256 and into scratch spills)
 				const bool hoist = HOIST && !STAB && t.seg_eff_off[seg + 1] - e0 == 1 && (task.z == 1 || t.seg_nh[seg] == 1);
 				if (hoist) load_eff(t, t.seg_effs[e0], TG, s, t.seg_hw + t.seg_hw_off[seg] + t.seg_eff_hoff[e0], pre);
-				// The two-wave build hoists only the effector's bone-direction basis (its nine
-				// device-memory loads per bone-step; C3 4.15 -> 4.08 ms).
-				const bool dbh = !HOIST && !STAB && !(kNoDbhPl2 && PL == 2) && t.seg_eff_off[seg + 1] - e0 == 1;
+				// (kDbh: the two-wave build may hoist only the effector's bone-direction basis;
+				// off by default since round 2, see kDbh)
+				const bool dbh = kDbh && !HOIST && !STAB && t.seg_eff_off[seg + 1] - e0 == 1;
 				if (dbh) pre.Db = ld_soa_basis<TL>(t, t.D, t.eff_bone[t.seg_effs[e0]], 9, 0, s);
 				for (int k = t.seg_bone_off[seg]; k < t.seg_bone_off[seg + 1]; k++)
 					bone_step<STAB, kPathReuse && (HOIST || (PL == 2 && !kNoPrPl2) || kPathReuse2W)>(t, seg, k, task.y, task.z, s, L, G, TG, ST, SF, HS, OE, MS, prev_dev, pre, hoist, dbh MBIK_PROF_ARG);
