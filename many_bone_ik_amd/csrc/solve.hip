@@ -133,47 +133,38 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void *base, uin
 template <class T>
 struct BRef {
 	__amdgpu_buffer_rsrc_t r;
-	uint32_t o;  // per-lane byte offset (VGPR)
-	uint32_t so; // wave-uniform byte offset (the instruction's SGPR offset field)
+	uint32_t o;
 	__device__ __forceinline__ operator T() const {
 		static_assert(sizeof(T) == 4 || sizeof(T) == 8, "32- or 64-bit elements");
-		if constexpr (sizeof(T) == 4) return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, o, so, 0));
-		else return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, o, so, 0));
+		if constexpr (sizeof(T) == 4) return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, o, 0, 0));
+		else return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, o, 0, 0));
 	}
 	__device__ __forceinline__ const BRef &operator=(T v) const {
-		if constexpr (sizeof(T) == 4) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, o, so, 0);
+		if constexpr (sizeof(T) == 4) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, o, 0, 0);
 		else {
 			typedef unsigned int U2 __attribute__((ext_vector_type(2)));
-			__builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(U2, v), r, o, so, 0);
+			__builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(U2, v), r, o, 0, 0);
 		}
 		return *this;
 	}
 };
-// The per-skeleton state areas (TG, ST, HS, ...) sit at wave-uniform distances from the
-// skeleton's base offset: those go to the SGPR offset (uplus), so every state pointer of a lane
-// shares one VGPR.
 template <class T>
 struct BPtr {
 	__amdgpu_buffer_rsrc_t r;
-	uint32_t o, so;
-	__device__ __forceinline__ BPtr operator+(int i) const { return BPtr{r, o + (uint32_t)(i * (int)sizeof(T)), so}; }
+	uint32_t o;
+	__device__ __forceinline__ BPtr operator+(int i) const { return BPtr{r, o + (uint32_t)(i * (int)sizeof(T))}; }
 	__device__ __forceinline__ BPtr &operator+=(int i) {
 		o += (uint32_t)(i * (int)sizeof(T));
 		return *this;
 	}
-	__device__ __forceinline__ BRef<T> operator[](int i) const { return BRef<T>{r, o + (uint32_t)(i * (int)sizeof(T)), so}; }
+	__device__ __forceinline__ BRef<T> operator[](int i) const { return BRef<T>{r, o + (uint32_t)(i * (int)sizeof(T))}; }
 };
-// p + k for a wave-uniform k
-template <class T>
-__device__ __forceinline__ T *uplus(T *p, int k) { return p + k; }
-template <class T>
-__device__ __forceinline__ BPtr<T> uplus(BPtr<T> p, int k) { return BPtr<T>{p.r, p.o, p.so + (uint32_t)(k * (int)sizeof(T))}; }
 // The same element type change for raw and buffer pointers (the staged headings' fp64
 // exchange slots, the int flags after the float state).
 template <class T, class U>
 __device__ __forceinline__ T *rebind(U *p) { return reinterpret_cast<T *>(p); }
 template <class T, class U>
-__device__ __forceinline__ BPtr<T> rebind(BPtr<U> p) { return BPtr<T>{p.r, p.o, p.so}; }
+__device__ __forceinline__ BPtr<T> rebind(BPtr<U> p) { return BPtr<T>{p.r, p.o}; }
 // float4 quads through either kind of pointer
 __device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
 __device__ __forceinline__ void st4(float *p, float4 v) { *reinterpret_cast<float4 *>(p) = v; }
@@ -1244,23 +1235,23 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 	LV L;
 	FP G;
 	const size_t loc0 = (s / kLocTile) * (size_t)(12 * kLocTile) * B + (s % kLocTile) * 4;
-	if constexpr (PL == 2) L.p = BPtr<float>{buf_rsrc(t.Lg, t.lg_bytes), (uint32_t)(loc0 * sizeof(float)), 0u};
+	if constexpr (PL == 2) L.p = BPtr<float>{buf_rsrc(t.Lg, t.lg_bytes), (uint32_t)(loc0 * sizeof(float))};
 	else if constexpr (PL == 1) L.p = t.Lg + loc0;
 	if constexpr (PL == 2) {
-		G = BPtr<float>{buf_rsrc(t.Sg, t.sg_bytes), (uint32_t)(s * (size_t)t.state_stride * sizeof(float)), 0u};
+		G = BPtr<float>{buf_rsrc(t.Sg, t.sg_bytes), (uint32_t)(s * (size_t)t.state_stride * sizeof(float))};
 	} else if constexpr (PL == 1) {
 		G = lds + (size_t)g * t.lds_stride;
 	} else {
 		L.p = lds + (size_t)g * t.lds_stride;
 		G = L.p + 12 * B;
 	}
-	const FP TG = uplus(G, 12 * t.n_gck);
-	const FP ST = uplus(TG, 12 * P);
-	const FP HS = uplus(ST, 12 * P);                  // staged headings (t.seg_hbase), 16-B aligned
-	const IP SF = rebind<int>(uplus(HS, t.hs_floats));
+	const FP TG = G + 12 * t.n_gck;
+	const FP ST = TG + 12 * P;
+	const FP HS = ST + 12 * P;                        // staged headings (t.seg_hbase), 16-B aligned
+	const IP SF = rebind<int>(HS + t.hs_floats);
 	constexpr bool TL = PL == 2; // placement 2 reads the tiled table copy
-	const FP OE = rebind<float>(uplus(SF, P));        // stabilization only: 3 per pin
-	const FP MS = uplus(OE, 3 * P);                  // stabilization only: 7 per pin
+	const FP OE = rebind<float>(SF + P);              // stabilization only: 3 per pin
+	const FP MS = OE + 3 * P;                        // stabilization only: 7 per pin
 	if (valid) {
 		for (int b = role; b < B; b += K)
 			if (t.bone_flags[b] & mbik::BF_IN_LIST) L.st(b, pose_to_xform(pose_in + ((size_t)local * B + b) * 10));
