@@ -586,6 +586,11 @@ constexpr bool kPathReuse = true;
 // segment (round 1: C3 -2 %).  With the state addressing and path sharing of round 2 those nine
 // registers spilled instead (placement 2: 31 spilled registers with them, 22 without), and
 // reading the basis at each step is faster: C3 -1 %, C4 -1.6 %, C5 -3 % (same-box A/B).
+#ifdef MBIK_NO_EFF_HOIST
+constexpr bool kEffHoist = false; // A/B switch: the one-wave build's per-segment effector data
+#else
+constexpr bool kEffHoist = true;
+#endif
 #ifdef MBIK_DBH
 constexpr bool kDbh = true; // A/B switch
 #else
@@ -1283,7 +1288,7 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 				EffPre pre;
 				// (not in the two-waves-per-SIMD build: the hoisted data's ~66 registers are what
 				// push that build past 256 and into scratch spills)
-				const bool hoist = HOIST && !STAB && t.seg_eff_off[seg + 1] - e0 == 1 && (task.z == 1 || t.seg_nh[seg] == 1);
+				const bool hoist = HOIST && kEffHoist && !STAB && t.seg_eff_off[seg + 1] - e0 == 1 && (task.z == 1 || t.seg_nh[seg] == 1);
 				if (hoist) load_eff(t, t.seg_effs[e0], TG, s, t.seg_hw + t.seg_hw_off[seg] + t.seg_eff_hoff[e0], pre);
 				// (kDbh: the two-wave build may hoist only the effector's bone-direction basis;
 				// off by default since round 2, see kDbh)
