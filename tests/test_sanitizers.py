@@ -4,6 +4,7 @@ builder -- ManyBoneIK3D::_bone_list_changed's segmentation and heading weights
 and every launch schedule build_schedule can produce -- and the oracle (object graph, one frame
 on 1 and 3 threads), on C1-C5 and the edge topologies of the GPU edge-case tests.  The
 drivers and their Makefile are in tools/san/; they build with g++/gcc (no GPU needed)."""
+import fcntl
 import math
 import os
 import struct
@@ -48,7 +49,12 @@ def write_case(path, wl, constraint_mode=0, stab=0):
 
 @pytest.fixture(scope="module")
 def drivers():
-    r = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tools", "san")], capture_output=True, text=True)
+    # one make at a time: pytest-xdist workers each run this fixture, and a worker executing a
+    # driver while another relinks it fails with a PermissionError
+    os.makedirs(OUT, exist_ok=True)
+    with open(os.path.join(OUT, ".make.lock"), "w") as lock:
+        fcntl.flock(lock, fcntl.LOCK_EX)
+        r = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tools", "san")], capture_output=True, text=True)
     if r.returncode != 0:
         pytest.fail("sanitizer build failed:\n" + r.stderr[-3000:])
     return os.path.join(OUT, "plan_san"), os.path.join(OUT, "oracle_san")
