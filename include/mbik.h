@@ -155,6 +155,13 @@ int32_t mbik_plan_set_locals_placement(mbik_plan *plan, int32_t placement);
  * be resident at once.  -1: automatic (mbik_plan_autotune times both).  Plans with
  * stabilization passes always use 1.  Results do not depend on it. */
 int32_t mbik_plan_set_waves_per_simd(mbik_plan *plan, int32_t waves);
+/* How the solve addresses the per-skeleton setup tables (D, CF, CD).  0 (default): with
+ * 32-bit offsets from a buffer resource when every table is below 4 GiB, else with 64-bit
+ * element indices.  1: always 64-bit indices (state placement 0 only: placements 1 and 2 need
+ * the 32-bit form and return MBIK_EUNSUPPORTED, which mbik_plan_autotune skips).  Plans whose
+ * tables reach 4 GiB therefore solve in placement 0, and mbik_group_solve launches them on
+ * their own.  Results do not depend on it. */
+int32_t mbik_plan_set_table_addressing(mbik_plan *plan, int32_t wide);
 /* Re-derives the per-skeleton setup data (bone-direction frames, Kusudama cones, tangent
  * circles and twist frames -- what mbik_plan_create computes on the host from the setup
  * pose, ManyBoneIK3D::_bone_list_changed many_bone_ik_3d.cpp:1011-1068) on the GPU for

@@ -89,8 +89,8 @@ struct DevPlan {
 	const double *CD;
 	// The per-skeleton tables D / CF / CD are [item][field][N].  Launches with the whole state in
 	// device memory read a skeleton-tiled copy instead, [item][row_n/kRowTile][field][kRowTile]
-	// (row_n = N rounded up; row_at<true>): one lane group's skeletons x all fields of a slot
-	// are then whole cache lines.
+	// (row_n = N rounded up; row_at<kTabTiled>): one lane group's skeletons x all fields of a
+	// slot are then whole cache lines.
 	int row_n = 0;
 	// mbik_solve_checked: per-skeleton flag, 1 when any bone's solved basis was non-finite and
 	// was written as the identity rotation (ik_bone_3d.cpp:174-176); null otherwise.
@@ -232,29 +232,60 @@ using LocTiled = LocV<12 * kLocTile, 4 * kLocTile, PT>;
 #define MBIK_SOA_S(s) (s)
 #endif
 constexpr int kRowTile = 16;
-template <bool TL>
+// Table addressing (TA) of a launch:
+//   kTab64    the plan's own layout, 64-bit element indices: tables of any size
+//             (constraint_mode, and placement-0 plans whose tables reach 4 GiB);
+//   kTab32    the plan's own layout as a buffer resource: the base in SGPRs, the lane's part of
+//             the offset (item, skeleton) as one 32-bit VGPR, the field's part -- uniform, a
+//             multiple of N -- as the instruction's SGPR offset, so the fields of a row cost no
+//             per-field vector address arithmetic (64-bit adds before);
+//   kTabTiled the skeleton-tiled copy (placement-2 launches), addressed the same way.
+// The 32-bit forms need every table below 4 GiB (tables_fit_32, checked at launch selection;
+// placements 1 and 2 require it; mbik_plan_set_table_addressing can force kTab64).
+constexpr int kTab64 = 0, kTab32 = 1, kTabTiled = 2;
+template <int TA>
 __device__ __forceinline__ size_t row_at(const DevPlan &t, int item, int fields, int f, size_t s) {
-	if constexpr (TL)
+	if constexpr (TA == kTabTiled)
 		return (size_t)item * fields * t.row_n + (s / kRowTile) * (size_t)(fields * kRowTile) + (size_t)f * kRowTile + s % kRowTile;
 	else
 		return ((size_t)item * fields + f) * t.N + MBIK_SOA_S(s);
 }
-// TL: the tiled copy (placement-2 launches); the default is the plan's own layout
-template <bool TL = false>
+template <int TA, class T>
+__device__ __forceinline__ T soa_at(const DevPlan &t, const T *a, int item, int fields, int f, size_t s) {
+	if constexpr (TA == kTab64) {
+		return a[row_at<TA>(t, item, fields, f, s)];
+	} else {
+		const __amdgpu_buffer_rsrc_t r = buf_rsrc(a, 0xFFFFFFFFu);
+		const uint32_t s32 = (uint32_t)MBIK_SOA_S(s);
+		uint32_t lane, fo;
+		if constexpr (TA == kTabTiled) {
+			lane = (uint32_t)item * (uint32_t)fields * (uint32_t)t.row_n + (s32 / kRowTile) * (uint32_t)(fields * kRowTile) + s32 % kRowTile;
+			fo = (uint32_t)f * kRowTile;
+		} else {
+			lane = (uint32_t)item * (uint32_t)fields * (uint32_t)t.N + s32;
+			fo = (uint32_t)f * (uint32_t)t.N;
+		}
+		lane *= (uint32_t)sizeof(T);
+		fo *= (uint32_t)sizeof(T);
+		if constexpr (sizeof(T) == 4) return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, lane, fo, 0));
+		else return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, lane, fo, 0));
+	}
+}
+template <int TA = kTab64>
 __device__ __forceinline__ float soa(const DevPlan &t, const float *a, int item, int fields, int f, size_t s) {
-	return a[row_at<TL>(t, item, fields, f, s)];
+	return soa_at<TA>(t, a, item, fields, f, s);
 }
-template <bool TL = false>
+template <int TA = kTab64>
 __device__ __forceinline__ double soad(const DevPlan &t, const double *a, int item, int fields, int f, size_t s) {
-	return a[row_at<TL>(t, item, fields, f, s)];
+	return soa_at<TA>(t, a, item, fields, f, s);
 }
-template <bool TL = false>
+template <int TA = kTab64>
 __device__ __forceinline__ B3 ld_soa_basis(const DevPlan &t, const float *a, int item, int fields, int f0, size_t s) {
 	B3 b;
 #pragma unroll
 	for (int i = 0; i < 3; i++)
-		b.r[i] = v3(soa<TL>(t, a, item, fields, f0 + 3 * i, s), soa<TL>(t, a, item, fields, f0 + 3 * i + 1, s),
-				soa<TL>(t, a, item, fields, f0 + 3 * i + 2, s));
+		b.r[i] = v3(soa<TA>(t, a, item, fields, f0 + 3 * i, s), soa<TA>(t, a, item, fields, f0 + 3 * i + 1, s),
+				soa<TA>(t, a, item, fields, f0 + 3 * i + 2, s));
 	return b;
 }
 
@@ -392,15 +423,14 @@ struct EffPre {
 	float pr[3];
 	double hws[7];
 };
-template <class FP>
+template <int TA, class FP>
 __device__ __forceinline__ void load_eff(const DevPlan &t, int e, const FP TG, size_t s, const double *hw, EffPre &p,
 		const B3 *Db = nullptr) {
-	constexpr bool TL = std::is_same_v<FP, BPtr<float>>; // placement 2: the tiled table copy
 	p.e = e;
 	p.off = t.eff_path_off[e];
 	p.de = t.eff_path_off[e + 1] - p.off - 1;
 	p.T = ld_x(TG + 12 * e);
-	p.Db = Db ? *Db : ld_soa_basis<TL>(t, t.D, t.eff_bone[e], 9, 0, s);
+	p.Db = Db ? *Db : ld_soa_basis<TA>(t, t.D, t.eff_bone[e], 9, 0, s);
 	p.hws[0] = hw[0];
 	int k = 1;
 #pragma unroll
@@ -481,12 +511,12 @@ __device__ __forceinline__ void effector_headings(const DevPlan &t, const EffPre
 	}
 	heading_terms(p, E, oe, Gb.o, H);
 }
-template <class LV, class FP, class IP>
+template <int TA, class LV, class FP, class IP>
 __device__ __forceinline__ void effector_headings(const DevPlan &t, int e, int d0, const X3 &Gb, const LV &L,
 		const FP TG, const FP ST, const IP SF, size_t s, const double *hw, Headings &H, const FP OE,
 		int oe_mode = 0, const B3 *Db = nullptr, PathCk *pc = nullptr, const int *lcp = nullptr) {
 	EffPre p;
-	load_eff(t, e, TG, s, hw, p, Db);
+	load_eff<TA>(t, e, TG, s, hw, p, Db);
 	effector_headings(t, p, d0, Gb, L, ST, SF, H, OE, oe_mode, pc, lcp);
 }
 
@@ -613,7 +643,7 @@ constexpr bool kPathReuse2W = false;
 #define MBIK_LIMITS_ATTR
 #endif
 // IKKusudama3D::get_local_point_in_limits (ik_kusudama_3d.cpp:273-332)
-template <bool TL = false>
+template <int TA = kTab64>
 __device__ MBIK_LIMITS_ATTR V3 local_point_in_limits(const DevPlan &t, int slot, size_t s, V3 in_point, double &in_bounds) {
 	const int nc = t.cons_ncones[slot];
 	V3 point = normalized(in_point);
@@ -623,9 +653,9 @@ __device__ MBIK_LIMITS_ATTR V3 local_point_in_limits(const DevPlan &t, int slot,
 	const V3 npoint = normalized(point); // closest_to_cone's input.normalized(), the same for every cone
 	for (int i = 0; i < nc; i++) {
 		const int o = mbik::CF_CONE0 + mbik::CF_PER_CONE * i;
-		auto f = [&](int k) { return soa<TL>(t, t.CF, slot, t.cf_stride, o + k, s); };
+		auto f = [&](int k) { return soa<TA>(t, t.CF, slot, t.cf_stride, o + k, s); };
 		V3 ncp = v3(f(mbik::CFC_NCP), f(mbik::CFC_NCP + 1), f(mbik::CFC_NCP + 2));
-		double rcos = soad<TL>(t, t.CD, slot, t.cd_stride, mbik::CD_PER_CONE * i, s);
+		double rcos = soad<TA>(t, t.CD, slot, t.cd_stride, mbik::CD_PER_CONE * i, s);
 		V3 c = closest_to_cone(ncp, f(mbik::CFC_SR), f(mbik::CFC_CR), rcos, npoint, in_bounds);
 		if (is_nan3(c)) {
 			in_bounds = 1;
@@ -640,9 +670,9 @@ __device__ MBIK_LIMITS_ATTR V3 local_point_in_limits(const DevPlan &t, int slot,
 	if (in_bounds == -1) {
 		for (int i = 0; i + 1 < nc; i++) {
 			const int o = mbik::CF_CONE0 + mbik::CF_PER_CONE * i;
-			auto f = [&](int k) { return soa<TL>(t, t.CF, slot, t.cf_stride, k, s); };
+			auto f = [&](int k) { return soa<TA>(t, t.CF, slot, t.cf_stride, k, s); };
 			auto f3 = [&](int k) { return v3(f(o + k), f(o + k + 1), f(o + k + 2)); };
-			double trcos = soad<TL>(t, t.CD, slot, t.cd_stride, mbik::CD_PER_CONE * i + 1, s);
+			double trcos = soad<TA>(t, t.CD, slot, t.cd_stride, mbik::CD_PER_CONE * i + 1, s);
 			V3 c = great_tangent_triangle(f3(mbik::CFC_C1XC2), f3(mbik::CFC_A1), f3(mbik::CFC_A2), f3(mbik::CFC_B1),
 					f3(mbik::CFC_B2), f3(mbik::CFC_T1), f3(mbik::CFC_T2), f(o + mbik::CFC_ST), f(o + mbik::CFC_CT), trcos, point);
 			if (isnan(c.x)) continue;
@@ -695,10 +725,9 @@ __device__ __forceinline__ void qcp_terms(const V3 wc1, const V3 c1, const V3 c2
 // STAB: the plan has stabilization passes (a separate instantiation keeps the retry loop and
 // its LDS staging out of the default kernel).
 // PR: reuse effector path prefixes (PathCk) in multi-effector segments solved from registers.
-template <bool STAB, bool PR, class LV, class FP, class IP>
+template <bool STAB, bool PR, int TA, class LV, class FP, class IP>
 __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j, int m, size_t s, const LV &L, const FP G, const FP TG,
 		const FP ST, const IP SF, const FP HS, const FP OE, const FP MS, double &prev_dev, const EffPre &pre, bool hoist, bool dbh MBIK_PROF_PARAM) {
-	constexpr bool TL = std::is_same_v<FP, BPtr<float>>; // placement 2: the tiled table copy
 	MBIK_PROF_T(pt0);
 #ifdef MBIK_PROF
 	uint64_t pt1 = pt0, pt3 = pt0;
@@ -741,7 +770,7 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 	if (nh == 1) {
 		// one heading in the segment: every lane of the group computes it (qcp.cpp:59-78)
 		if (hoist) effector_headings(t, pre, d0, Gb, L, ST, SF, H, OE, oe_mode);
-		else effector_headings(t, t.seg_effs[e0], d0, Gb, L, TG, ST, SF, s, hw, H, OE, oe_mode, dbh ? &pre.Db : nullptr);
+		else effector_headings<TA>(t, t.seg_effs[e0], d0, Gb, L, TG, ST, SF, s, hw, H, OE, oe_mode, dbh ? &pre.Db : nullptr);
 		V3 mvd = H.hm[0], tgt = H.ht[0];
 		if (translate) {
 			double w = H.w[0];
@@ -769,7 +798,7 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 			pc.d = -1;
 			for (int i = e0; i < e1; i++) {
 				if (hoist) effector_headings(t, pre, d0, Gb, L, ST, SF, H, OE, oe_mode);
-				else effector_headings(t, t.seg_effs[i], d0, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, oe_mode,
+				else effector_headings<TA>(t, t.seg_effs[i], d0, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, oe_mode,
 						dbh ? &pre.Db : nullptr, PR ? &pc : nullptr, t.seg_eff_lcp + i);
 #pragma unroll
 				for (int h = 0; h < 7; h++) {
@@ -793,7 +822,7 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 		for (int i = e0; i < e1; i++) {
 			MBIK_PROF_T(ph1);
 			if (hoist) effector_headings(t, pre, d0, Gb, L, ST, SF, H, OE, oe_mode);
-			else effector_headings(t, t.seg_effs[i], d0, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, oe_mode,
+			else effector_headings<TA>(t, t.seg_effs[i], d0, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, oe_mode,
 					dbh ? &pre.Db : nullptr, PR ? &pc : nullptr, t.seg_eff_lcp + i);
 			MBIK_PROF_T(ph2);
 			MBIK_PROF_ADD(9, ph1, ph2);
@@ -840,7 +869,7 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 		const auto ex = rebind<double>(hsg + HS_REC * nh);
 		for (int i = e0 + j; i < e1; i += m) {
 			MBIK_PROF_T(ph1);
-			effector_headings(t, t.seg_effs[i], d0, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, oe_mode);
+			effector_headings<TA>(t, t.seg_effs[i], d0, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, oe_mode);
 			MBIK_PROF_T(ph2);
 			MBIK_PROF_ADD(9, ph1, ph2);
 			auto r = hsg + HS_REC * t.seg_eff_hoff[i];
@@ -1022,7 +1051,7 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 		Headings H;
 		const double *hw = t.seg_hw + t.seg_hw_off[seg];
 		for (int i = t.seg_eff_off[seg] + j; i < t.seg_eff_off[seg + 1]; i += m)
-			effector_headings(t, t.seg_effs[i], d0, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, 1);
+			effector_headings<TA>(t, t.seg_effs[i], d0, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, 1);
 	}
 
 	MBIK_PROF_T(pt2);
@@ -1043,13 +1072,13 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 		X3 Gs = P * Lb;
 		GsB = Gs.b;
 		gs_ok = true;
-		Gbd_stale.b = Gs.b * ld_soa_basis<TL>(t, t.D, b, 9, 0, s);
+		Gbd_stale.b = Gs.b * ld_soa_basis<TA>(t, t.D, b, 9, 0, s);
 		Gbd_stale.o = Gs.o;
 		X3 Gco = {P.b, xform(P, Lb.o)}; // constraint_orientation: (I, pose local origin) under the parent
 		V3 bdx = xform(Gbd_stale, v3(0.0f, 1.0f, 0.0f));
 		V3 tip = xform(X3{Pinv, xform(Pinv, -Gco.o)}, bdx); // Gco.basis == P.basis
 		double in_bounds = 1.0;
-		V3 inl = local_point_in_limits<TL>(t, slot, s, tip, in_bounds);
+		V3 inl = local_point_in_limits<TA>(t, slot, s, tip, in_bounds);
 		if (in_bounds < 0) {
 			V3 p2 = xform(Gco, inl);
 			Q rect = arc(bdx - Gco.o, p2 - Gco.o);
@@ -1067,10 +1096,10 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 	if (flags & mbik::BF_AXIAL) {
 #endif
 		const int cs = t.cf_stride;
-		Q tcr = q4(soa<TL>(t, t.CF, slot, cs, mbik::CF_TWIST_Q, s), soa<TL>(t, t.CF, slot, cs, mbik::CF_TWIST_Q + 1, s),
-				soa<TL>(t, t.CF, slot, cs, mbik::CF_TWIST_Q + 2, s), soa<TL>(t, t.CF, slot, cs, mbik::CF_TWIST_Q + 3, s));
-		float half_cos = soa<TL>(t, t.CF, slot, cs, mbik::CF_TWIST_COS, s);
-		B3 Tb = ld_soa_basis<TL>(t, t.CF, slot, cs, mbik::CF_TWIST_T, s);
+		Q tcr = q4(soa<TA>(t, t.CF, slot, cs, mbik::CF_TWIST_Q, s), soa<TA>(t, t.CF, slot, cs, mbik::CF_TWIST_Q + 1, s),
+				soa<TA>(t, t.CF, slot, cs, mbik::CF_TWIST_Q + 2, s), soa<TA>(t, t.CF, slot, cs, mbik::CF_TWIST_Q + 3, s));
+		float half_cos = soa<TA>(t, t.CF, slot, cs, mbik::CF_TWIST_COS, s);
+		B3 Tb = ld_soa_basis<TA>(t, t.CF, slot, cs, mbik::CF_TWIST_T, s);
 		B3 Gct = P.b * Tb;
 		X3 Gs;
 		if (gs_ok && !swung) Gs.b = GsB;
@@ -1105,7 +1134,7 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 		Headings H;
 		for (int i = t.seg_eff_off[seg] + j; i < t.seg_eff_off[seg + 1]; i += m) {
 			const int e = t.seg_effs[i];
-			effector_headings(t, e, d0, Gnow, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, 2);
+			effector_headings<TA>(t, e, d0, Gnow, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, 2);
 #pragma unroll
 			for (int h = 0; h < 7; h++) {
 				if (H.mask & (1 << h)) {
@@ -1193,7 +1222,7 @@ __device__ __forceinline__ void write_nonfinite(const DevPlan &t, bool valid, bo
 #define MBIK_WAVES_PER_EU 1
 #endif
 // The solve of one block (blk = the plan-local block index after the XCD remap).
-template <bool STAB, int PL, bool HOIST = true>
+template <bool STAB, int PL, bool HOIST = true, bool T32 = true>
 __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int count, const float *__restrict__ pose_in,
 		const float *__restrict__ targets, float *__restrict__ pose_out, int iterations, int seg_lo, int seg_hi) {
 	extern __shared__ float4 lds4[];
@@ -1254,7 +1283,7 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 	const FP ST = TG + 12 * P;
 	const FP HS = ST + 12 * P;                        // staged headings (t.seg_hbase), 16-B aligned
 	const IP SF = rebind<int>(HS + t.hs_floats);
-	constexpr bool TL = PL == 2; // placement 2 reads the tiled table copy
+	constexpr int TA = PL == 2 ? kTabTiled : (T32 ? kTab32 : kTab64); // placement 2 reads the tiled table copy
 	const FP OE = rebind<float>(SF + P);              // stabilization only: 3 per pin
 	const FP MS = OE + 3 * P;                        // stabilization only: 7 per pin
 	if (valid) {
@@ -1289,13 +1318,13 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 				// (not in the two-waves-per-SIMD build: the hoisted data's ~66 registers are what
 				// push that build past 256 and into scratch spills)
 				const bool hoist = HOIST && kEffHoist && !STAB && t.seg_eff_off[seg + 1] - e0 == 1 && (task.z == 1 || t.seg_nh[seg] == 1);
-				if (hoist) load_eff(t, t.seg_effs[e0], TG, s, t.seg_hw + t.seg_hw_off[seg] + t.seg_eff_hoff[e0], pre);
+				if (hoist) load_eff<TA>(t, t.seg_effs[e0], TG, s, t.seg_hw + t.seg_hw_off[seg] + t.seg_eff_hoff[e0], pre);
 				// (kDbh: the two-wave build may hoist only the effector's bone-direction basis;
 				// off by default since round 2, see kDbh)
 				const bool dbh = kDbh && !HOIST && !STAB && t.seg_eff_off[seg + 1] - e0 == 1;
-				if (dbh) pre.Db = ld_soa_basis<TL>(t, t.D, t.eff_bone[t.seg_effs[e0]], 9, 0, s);
+				if (dbh) pre.Db = ld_soa_basis<TA>(t, t.D, t.eff_bone[t.seg_effs[e0]], 9, 0, s);
 				for (int k = t.seg_bone_off[seg]; k < t.seg_bone_off[seg + 1]; k++)
-					bone_step<STAB, kPathReuse && (HOIST || (PL == 2 && !kNoPrPl2) || kPathReuse2W)>(t, seg, k, task.y, task.z, s, L, G, TG, ST, SF, HS, OE, MS, prev_dev, pre, hoist, dbh MBIK_PROF_ARG);
+					bone_step<STAB, kPathReuse && (HOIST || (PL == 2 && !kNoPrPl2) || kPathReuse2W), TA>(t, seg, k, task.y, task.z, s, L, G, TG, ST, SF, HS, OE, MS, prev_dev, pre, hoist, dbh MBIK_PROF_ARG);
 			}
 			__syncthreads();
 		}
@@ -1340,10 +1369,10 @@ __device__ __forceinline__ int xcd_block() {
 // file, no spills.  2: at most 256 registers, some spilled to scratch, but two one-wave
 // blocks share a SIMD -- for launches whose skeletons no longer fit the chip at once and
 // whose state is not in LDS (mbik_plan_set_waves_per_simd; autotune decides).
-template <bool STAB, int PL, int WPE = MBIK_WAVES_PER_EU>
+template <bool STAB, int PL, int WPE = MBIK_WAVES_PER_EU, bool T32 = true>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void mbik_solve_kernel(DevPlan t, int first, int count, const float *__restrict__ pose_in,
 		const float *__restrict__ targets, float *__restrict__ pose_out, int iterations, int seg_lo, int seg_hi) {
-	solve_block<STAB, PL, WPE == 1>(t, xcd_block(), first, count, pose_in, targets, pose_out, iterations, seg_lo, seg_hi);
+	solve_block<STAB, PL, WPE == 1, T32>(t, xcd_block(), first, count, pose_in, targets, pose_out, iterations, seg_lo, seg_hi);
 }
 
 // A heterogeneous batch (mbik_group_solve): several plans -- distinct rigs -- in one launch.
@@ -1458,6 +1487,7 @@ struct mbik_plan {
 	double alg_flops = 0;
 	int sched_K = -1, sched_c = -1, sched_staging = -1; // layout of the uploaded topology blob
 	int staging_override = -1;                           // mbik_plan_set_heading_staging; -1 = automatic
+	int tab64 = 0;                                       // mbik_plan_set_table_addressing
 	int locals_override = -1;                            // mbik_plan_set_locals_placement; -1 = automatic
 	int waves_override = -1;                             // mbik_plan_set_waves_per_simd; -1 = automatic
 	int sched_locals = -1;
@@ -1552,19 +1582,40 @@ int upload_topology(mbik_plan *p) {
 }
 
 using SolveKernel = void (*)(DevPlan, int, int, const float *, const float *, float *, int, int, int);
-// The solve kernel instantiation of a plan's current layout (stabilization x locals placement).
-SolveKernel solve_kernel_for(const mbik::HostPlan &h) {
+// device-memory areas addressed through buffer resources (32-bit byte offsets): the state of
+// placements 1 and 2, and the setup tables of every layout that can (kTab32 / kTabTiled)
+constexpr size_t kMaxBufBytes = 0xFFFFFFF0u;
+// Every setup table (D, CF, CD, and their skeleton-tiled copies, sized for the padded N) below
+// 4 GiB: the solve can address them with 32-bit offsets.  Placement-0 plans beyond that run
+// the 64-bit-index instantiation; placements 1 and 2 require it.
+bool tables_fit_32(const mbik_plan *p) {
+	const mbik::HostPlan &h = p->host;
+	if (p->tab64) return false;
+	const size_t n = (size_t)(h.N + kRowTile - 1) / kRowTile * kRowTile;
+	return (size_t)h.B * 9 * n * sizeof(float) <= kMaxBufBytes && (size_t)h.NC * h.cf_stride() * n * sizeof(float) <= kMaxBufBytes &&
+			(size_t)h.NC * h.cd_stride() * n * sizeof(double) <= kMaxBufBytes;
+}
+// The solve kernel instantiation of a plan's current layout (stabilization x locals placement
+// x waves per SIMD, and for placement 0 the table addressing).
+SolveKernel solve_kernel_for(const mbik_plan *p) {
+	const mbik::HostPlan &h = p->host;
 	static const SolveKernel ks[2][3] = {{mbik_solve_kernel<false, 0>, mbik_solve_kernel<false, 1>, mbik_solve_kernel<false, 2>},
 			{mbik_solve_kernel<true, 0>, mbik_solve_kernel<true, 1>, mbik_solve_kernel<true, 2>}};
 	static const SolveKernel k2[3] = {mbik_solve_kernel<false, 0, 2>, mbik_solve_kernel<false, 1, 2>, mbik_solve_kernel<false, 2, 2>};
+	// placement 0 with tables of 4 GiB or more: 64-bit element indices
+	static const SolveKernel k64[3] = {mbik_solve_kernel<false, 0, 1, false>, mbik_solve_kernel<true, 0, 1, false>,
+			mbik_solve_kernel<false, 0, 2, false>};
 	static std::once_flag once;
 	std::call_once(once, [] {
 		for (auto &row : ks)
 			for (SolveKernel k : row) (void)hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 		for (SolveKernel k : k2) (void)hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+		for (SolveKernel k : k64) (void)hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 	});
 	const int pl = std::min(2, std::max(0, (int)h.state_hbm));
-	if (h.waves_per_simd == 2 && h.stabilization_passes == 0) return k2[pl];
+	const bool two = h.waves_per_simd == 2 && h.stabilization_passes == 0;
+	if (pl == 0 && !tables_fit_32(p)) return two ? k64[2] : k64[h.stabilization_passes > 0 ? 1 : 0];
+	if (two) return k2[pl];
 	return ks[h.stabilization_passes > 0 ? 1 : 0][pl];
 }
 
@@ -1573,7 +1624,7 @@ SolveKernel solve_kernel_for(const mbik::HostPlan &h) {
 int blocks_per_cu(void *ctx, int64_t lds_bytes) {
 	const mbik_plan *p = static_cast<const mbik_plan *>(ctx);
 	int n = 0;
-	const void *k = (const void *)solve_kernel_for(p->host);
+	const void *k = (const void *)solve_kernel_for(p);
 	if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, 64, (size_t)lds_bytes) != hipSuccess || n <= 0)
 		return (int)(160 * 1024 / std::max<int64_t>(1, lds_bytes));
 	return n;
@@ -1583,9 +1634,6 @@ int blocks_per_cu(void *ctx, int64_t lds_bytes) {
 // cheap and its state lives in HBM, so the chip's VALU issue (many narrow waves), not one
 // skeleton's chain, bounds it beyond that (C2 / C3 / C5: DESIGN.md §1, profiles/r01_cmode_lanes_sweep.jsonl).
 constexpr int kCmodeLanes = 4;
-// device-memory state areas are addressed through buffer resources (32-bit byte offsets)
-constexpr size_t kMaxBufBytes = 0xFFFFFFF0u;
-
 int ensure_schedule(mbik_plan *p, int64_t nlaunch) {
 	mbik::HostPlan &h = p->host;
 	int lanes = p->lanes_override;
@@ -1593,6 +1641,8 @@ int ensure_schedule(mbik_plan *p, int64_t nlaunch) {
 	h.staging = p->staging_override != 0;
 	h.state_hbm = h.constraint_mode ? 0 : std::max(0, p->locals_override);
 	h.waves_per_simd = (p->waves_override == 2 && !h.constraint_mode && h.stabilization_passes == 0) ? 2 : 1;
+	if (h.state_hbm >= 1 && !tables_fit_32(p))
+		return fail(MBIK_EUNSUPPORTED, "state placements 1 and 2 need every setup table < 4 GiB (fewer skeletons per plan)");
 	if (h.state_hbm >= 1 && !p->d_locals) {
 		// LocTiled: whole tiles of kLocTile skeletons
 		const size_t bytes = (size_t)((h.N + kLocTile - 1) / kLocTile) * kLocTile * h.B * 12 * sizeof(float);
@@ -1795,7 +1845,7 @@ int launch(mbik_plan *p, int first, int count, const float *pose_in, const float
 #endif
 	if (lds > 160 * 1024) return fail(MBIK_EUNSUPPORTED, "skeleton too large for LDS at this lane count");
 	unsigned blocks = (unsigned)((count + h.spw - 1) / h.spw);
-	auto kern = solve_kernel_for(h);
+	auto kern = solve_kernel_for(p);
 	DevPlan d = p->dev;
 	if (h.state_hbm == 2) {
 		if ((rc = ensure_tiled_rows(p, stream)) != MBIK_OK) return rc;
@@ -2428,6 +2478,14 @@ int32_t mbik_plan_set_waves_per_simd(mbik_plan *p, int32_t waves) {
 	return MBIK_OK;
 }
 
+int32_t mbik_plan_set_table_addressing(mbik_plan *p, int32_t wide) {
+	if (!p) return fail(MBIK_EINVAL, "null plan");
+	if (wide != 0 && wide != 1) return fail(MBIK_EINVAL, "table addressing must be 0 (automatic) or 1 (64-bit indices)");
+	p->tab64 = wide;
+	p->sched_K = -1;
+	return MBIK_OK;
+}
+
 int32_t mbik_plan_set_locals_placement(mbik_plan *p, int32_t placement) {
 	if (!p) return fail(MBIK_EINVAL, "null plan");
 	if (placement < -1 || placement > 2)
@@ -3045,9 +3103,10 @@ int32_t mbik_group_solve(mbik_group *g, const int32_t *first, const int32_t *cou
 		if (!pose_in[i] || !pose_out[i] || (p->host.P > 0 && !targets[i])) return fail(MBIK_EINVAL, "null buffer");
 		int rc = p->host.P > 0 ? ensure_schedule(p, c) : MBIK_OK;
 		if (rc) return rc;
-		if (p->host.constraint_mode || p->host.P == 0 || p->host.state_hbm != 0) {
+		if (p->host.constraint_mode || p->host.P == 0 || p->host.state_hbm != 0 || !tables_fit_32(p)) {
 			// constraint_mode plans have their own kernel, so do plans laid out with their
-			// locals in HBM; pinless plans only copy
+			// locals in HBM and plans whose setup tables need 64-bit indices; pinless plans
+			// only copy
 			rc = launch(p, f, c, pose_in[i], targets[i], pose_out[i], stream, p->host.iterations, 0, p->host.NS - 1);
 			if (rc) return rc;
 			continue;

@@ -219,6 +219,10 @@ class Plan:
         """mbik_plan_set_waves_per_simd: 1 or 2 waves per SIMD, -1 automatic."""
         check(self._L.mbik_plan_set_waves_per_simd(self.h, int(waves)))
 
+    def set_table_addressing(self, wide: int = 0):
+        """mbik_plan_set_table_addressing: 0 automatic (32-bit offsets below 4 GiB), 1 64-bit indices."""
+        check(self._L.mbik_plan_set_table_addressing(self.h, int(wide)))
+
     def autotune(self, pose_in_ptr: int, targets_ptr: int, pose_out_ptr: int, first: int = 0,
                  count: int | None = None, stream: int = 0):
         """mbik_plan_autotune: time candidate layouts on this batch, keep the fastest."""

@@ -179,6 +179,41 @@ def test_two_waves_per_simd_bitwise_vs_oracle(oracle, mbik, cfg, n, placement):
     assert_parity(plan.solve_host(wl.pose, wl.targets), ref, f"C{cfg} 2 waves/SIMD placement {placement}")
 
 
+@pytest.mark.parametrize("cfg,n", [(2, 48), (4, 16), (5, 6)])
+@pytest.mark.parametrize("waves", [1, 2])
+def test_table_addressing_64bit_bitwise_vs_oracle(oracle, mbik, cfg, n, waves):
+    """mbik_plan_set_table_addressing(1): the instantiation with 64-bit table indices -- the
+    one plans whose setup tables reach 4 GiB run -- computes the same bits, placements 1 and 2
+    refuse it, and a fused group launches such a plan on its own."""
+    wl = W.generate(cfg, n, first=21000)
+    ref = oracle.Oracle(wl).solve(wl.pose, wl.targets, threads=8)
+    plan = Plan.from_workload(wl)
+    plan.set_table_addressing(1)
+    plan.set_waves_per_simd(waves)
+    assert_parity(plan.solve_host(wl.pose, wl.targets), ref, f"C{cfg} 64-bit table indices, {waves} waves/SIMD")
+    plan.set_locals_placement(1)
+    with pytest.raises(_lib.MbikError):
+        plan.solve_host(wl.pose, wl.targets)
+    plan.set_locals_placement(0)
+    if waves == 1 and cfg == 2:
+        import torch
+        from many_bone_ik_amd.solver import Group
+        wl3 = W.generate(3, 24, first=77)
+        ref3 = oracle.Oracle(wl3).solve(wl3.pose, wl3.targets, threads=8)
+        plan3 = Plan.from_workload(wl3)
+        grp = Group([plan, plan3])
+        dev = torch.device("cuda", 0)
+        pi, pi3 = torch.from_numpy(wl.pose).to(dev), torch.from_numpy(wl3.pose).to(dev)
+        tg, tg3 = torch.from_numpy(wl.targets).to(dev), torch.from_numpy(wl3.targets).to(dev)
+        po, po3 = torch.empty_like(pi), torch.empty_like(pi3)
+        grp.solve([pi.data_ptr(), pi3.data_ptr()], [tg.data_ptr(), tg3.data_ptr()], [po.data_ptr(), po3.data_ptr()])
+        torch.cuda.synchronize()
+        assert_parity(po.cpu().numpy(), ref, "group: 64-bit-table plan")
+        assert_parity(po3.cpu().numpy(), ref3, "group: 32-bit-table plan")
+    with pytest.raises(_lib.MbikError):
+        plan.set_table_addressing(2)
+
+
 def test_waves_argument_check(mbik):
     plan = Plan.from_workload(W.generate(3, 2))
     with pytest.raises(_lib.MbikError):
