@@ -214,6 +214,29 @@ def test_table_addressing_64bit_bitwise_vs_oracle(oracle, mbik, cfg, n, waves):
         plan.set_table_addressing(2)
 
 
+def test_tables_past_4gib_use_64bit_indices(oracle, mbik):
+    """A placement-0 plan whose constraint table passes 4 GiB (the C5 rig's CF is 60.5 KB per
+    skeleton: 72,000 skeletons make 4.36 GB) solves through the 64-bit-index kernel by itself,
+    and placement 1 refuses it.  The batch repeats 64 distinct skeletons, so the oracle's
+    results for those 64 check the first and the last 64 (the latter read table offsets past
+    2^32 bytes)."""
+    import dataclasses
+    base = W.generate(5, 64, first=333)
+    n = 72000
+    rep = n // 64
+    wl = dataclasses.replace(base, n=n, pose=np.tile(base.pose, (rep, 1, 1)), targets=np.tile(base.targets, (rep, 1, 1)),
+                             cones=np.tile(base.cones, (rep, 1, 1, 1)), twist=np.tile(base.twist, (rep, 1, 1)))
+    assert wl.pose.shape[0] == n and 199 * (14 + 31 * 2) * n * 4 > 2 ** 32
+    ref = oracle.Oracle(base).solve(base.pose, base.targets, threads=8)
+    plan = Plan.from_workload(wl)
+    got = plan.solve_host(wl.pose, wl.targets)
+    assert_parity(got[:64], ref, "C5 x 72,000 (tables > 4 GiB): first 64")
+    assert_parity(got[n - 64:], ref, "C5 x 72,000 (tables > 4 GiB): last 64")
+    plan.set_locals_placement(1)
+    with pytest.raises(_lib.MbikError):
+        plan.solve_host(base.pose[:1], base.targets[:1])
+
+
 def test_waves_argument_check(mbik):
     plan = Plan.from_workload(W.generate(3, 2))
     with pytest.raises(_lib.MbikError):
