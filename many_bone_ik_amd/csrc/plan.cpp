@@ -30,6 +30,7 @@ std::string build_topology(const mbik_skeleton_desc &desc, const mbik_config &cf
 	if (desc.pin_count < 0 || (desc.pin_count > 0 && !desc.pins)) return "invalid pins";
 	if (desc.constraint_count < 0 || (desc.constraint_count > 0 && !desc.constraints)) return "invalid constraints";
 	if (cfg.iterations_per_frame < 0) return "iterations_per_frame must be >= 0";
+	if (cfg.bone_damp_count < 0) return "negative count";
 	p.B = B;
 	p.P = desc.pin_count;
 	p.max_cones = std::max(1, desc.max_cones);

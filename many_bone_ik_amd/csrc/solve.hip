@@ -130,20 +130,53 @@ __device__ __forceinline__ void st_x(float *p, const X3 &t) {
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void *base, uint32_t bytes) {
 	return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, (int)bytes, 0x00020000);
 }
+// Diagnostic builds (never the shipped library):
+//   MBIK_CHECK_BOUNDS  every buffer-pointer access checks that it stays inside the area it was
+//                      derived from (one skeleton's state slice, or the whole locals area) and
+//                      inside the resource's records; the first violations are printed.
+//   MBIK_SOFF          the wave-uniform distance of a state area from the skeleton's slice
+//                      (TG, ST, HS, SF, OE, MS) goes to the instruction's SGPR offset instead of
+//                      the lane's VGPR offset (the round-2 experiment reverted in 395e810;
+//                      DESIGN.md §10 records why it is not shipped).
+struct BDiag {
+#ifdef MBIK_CHECK_BOUNDS
+	uint32_t lo = 0, hi = 0, n = 0; // [lo, hi): the area; n: the resource's records
+#endif
+};
+#ifdef MBIK_CHECK_BOUNDS
+__device__ unsigned int g_mbik_oob;
+__device__ __noinline__ void mbik_oob_report(const BDiag &d, uint32_t o, uint32_t so, uint32_t sz, int store) {
+	const unsigned int k = atomicAdd(&g_mbik_oob, 1u);
+	if (k < 24)
+		printf("mbik OOB %s: block %d lane %d voff %u soff %u size %u area [%u,%u) records %u\n", store ? "store" : "load",
+				(int)blockIdx.x, (int)threadIdx.x, o, so, sz, d.lo, d.hi, d.n);
+}
+__device__ __forceinline__ void mbik_bcheck(const BDiag &d, uint32_t o, uint32_t so, uint32_t sz, int store) {
+	const uint64_t a = (uint64_t)o + so;
+	if (a < d.lo || a + sz > d.hi || (uint64_t)o >= d.n || a + sz > d.n) mbik_oob_report(d, o, so, sz, store);
+}
+#define MBIK_BCHECK(d, o, so, sz, st) mbik_bcheck(d, o, so, sz, st)
+#else
+#define MBIK_BCHECK(d, o, so, sz, st)
+#endif
 template <class T>
 struct BRef {
 	__amdgpu_buffer_rsrc_t r;
-	uint32_t o;
+	uint32_t o;  // per-lane byte offset (VGPR)
+	uint32_t so; // wave-uniform byte offset (MBIK_SOFF only; 0 otherwise)
+	BDiag d;
 	__device__ __forceinline__ operator T() const {
 		static_assert(sizeof(T) == 4 || sizeof(T) == 8, "32- or 64-bit elements");
-		if constexpr (sizeof(T) == 4) return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, o, 0, 0));
-		else return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, o, 0, 0));
+		MBIK_BCHECK(d, o, so, sizeof(T), 0);
+		if constexpr (sizeof(T) == 4) return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, o, so, 0));
+		else return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, o, so, 0));
 	}
 	__device__ __forceinline__ const BRef &operator=(T v) const {
-		if constexpr (sizeof(T) == 4) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, o, 0, 0);
+		MBIK_BCHECK(d, o, so, sizeof(T), 1);
+		if constexpr (sizeof(T) == 4) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, o, so, 0);
 		else {
 			typedef unsigned int U2 __attribute__((ext_vector_type(2)));
-			__builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(U2, v), r, o, 0, 0);
+			__builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(U2, v), r, o, so, 0);
 		}
 		return *this;
 	}
@@ -151,20 +184,64 @@ struct BRef {
 template <class T>
 struct BPtr {
 	__amdgpu_buffer_rsrc_t r;
-	uint32_t o;
-	__device__ __forceinline__ BPtr operator+(int i) const { return BPtr{r, o + (uint32_t)(i * (int)sizeof(T))}; }
+	uint32_t o, so;
+	BDiag d;
+	__device__ __forceinline__ BPtr operator+(int i) const { return BPtr{r, o + (uint32_t)(i * (int)sizeof(T)), so, d}; }
 	__device__ __forceinline__ BPtr &operator+=(int i) {
 		o += (uint32_t)(i * (int)sizeof(T));
 		return *this;
 	}
-	__device__ __forceinline__ BRef<T> operator[](int i) const { return BRef<T>{r, o + (uint32_t)(i * (int)sizeof(T))}; }
+	__device__ __forceinline__ BRef<T> operator[](int i) const { return BRef<T>{r, o + (uint32_t)(i * (int)sizeof(T)), so, d}; }
 };
+// A buffer pointer to `bytes` bytes at base, at byte offset o; [lo, hi) bounds the accesses made
+// through it and its derivatives (MBIK_CHECK_BOUNDS only).
+template <class T>
+__device__ __forceinline__ BPtr<T> bptr(const void *base, uint32_t bytes, uint32_t o, uint32_t lo, uint32_t hi) {
+	BPtr<T> p{buf_rsrc(base, bytes), o, 0u, BDiag{}};
+#ifdef MBIK_CHECK_BOUNDS
+	p.d.lo = lo;
+	p.d.hi = hi;
+	p.d.n = bytes;
+#else
+	(void)lo;
+	(void)hi;
+#endif
+	return p;
+}
+// p + k for a wave-uniform k (a state area's distance from the skeleton's slice); `area`
+// selects which areas take the SGPR form under MBIK_SOFF (bit mask MBIK_SOFF, 1 = all).
+#ifdef MBIK_SOFF
+#if MBIK_SOFF == 1
+#define MBIK_SOFF_AREAS 0xFF
+#else
+#define MBIK_SOFF_AREAS MBIK_SOFF
+#endif
+#endif
+template <class T>
+__device__ __forceinline__ T *uplus(T *p, int k, int area = 0) {
+	(void)area;
+	return p + k;
+}
+template <class T>
+__device__ __forceinline__ BPtr<T> uplus(BPtr<T> p, int k, int area = 0xFF) {
+#ifdef MBIK_SOFF
+	if (area & MBIK_SOFF_AREAS) {
+#ifdef MBIK_SOFF_RFL
+		return BPtr<T>{p.r, p.o, (uint32_t)__builtin_amdgcn_readfirstlane((int)(p.so + (uint32_t)(k * (int)sizeof(T)))), p.d};
+#else
+		return BPtr<T>{p.r, p.o, p.so + (uint32_t)(k * (int)sizeof(T)), p.d};
+#endif
+	}
+#endif
+	(void)area;
+	return p + k;
+}
 // The same element type change for raw and buffer pointers (the staged headings' fp64
 // exchange slots, the int flags after the float state).
 template <class T, class U>
 __device__ __forceinline__ T *rebind(U *p) { return reinterpret_cast<T *>(p); }
 template <class T, class U>
-__device__ __forceinline__ BPtr<T> rebind(BPtr<U> p) { return BPtr<T>{p.r, p.o}; }
+__device__ __forceinline__ BPtr<T> rebind(BPtr<U> p) { return BPtr<T>{p.r, p.o, p.so, p.d}; }
 // float4 quads through either kind of pointer
 __device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
 __device__ __forceinline__ void st4(float *p, float4 v) { *reinterpret_cast<float4 *>(p) = v; }
@@ -458,6 +535,11 @@ struct PathCk {
 	X3 x;
 	int d;
 };
+#ifdef MBIK_FAN_RESET
+constexpr bool kFanKeep = false; // A/B switch: round 2's reset after every reuse
+#else
+constexpr bool kFanKeep = true;
+#endif
 template <class LV, class FP, class IP>
 __device__ __forceinline__ void effector_headings(const DevPlan &t, const EffPre &p, int d0, const X3 &Gb, const LV &L,
 		const FP ST, const IP SF, Headings &H, const FP OE, int oe_mode = 0, PathCk *pc = nullptr, const int *lcp = nullptr) {
@@ -486,17 +568,23 @@ __device__ __forceinline__ void effector_headings(const DevPlan &t, const EffPre
 		if (pc) {
 			// lcp[0]: depths shared with the previous effector; lcp[1]: with the next one
 			const int l = lcp[0];
+			const int cpd = lcp[1] - 1;
+			bool reused = false;
 			if (pc->d >= d0 && pc->d == l - 1) {
 				X = pc->x;
 				d = l;
+				reused = true;
 			}
-			pc->d = -1;
-			const int cpd = lcp[1] - 1;
-			if (cpd >= d && cpd <= de) {
-				walk(d, cpd);
-				pc->x = X;
-				pc->d = cpd;
-				d = cpd + 1;
+			// A fan of three or more effectors branching at one depth: the next one shares
+			// exactly the prefix just reused, so the checkpoint stays for it.
+			if (!(kFanKeep && reused && cpd == d - 1)) {
+				pc->d = -1;
+				if (cpd >= d && cpd <= de) {
+					walk(d, cpd);
+					pc->x = X;
+					pc->d = cpd;
+					d = cpd + 1;
+				}
 			}
 		}
 		walk(d, de);
@@ -710,6 +798,9 @@ __device__ __forceinline__ void wave_sync_lds() {
 	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 	__builtin_amdgcn_wave_barrier();
 	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#ifdef MBIK_SYNC_CLOBBER
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // diagnostic: a hard ordering point
+#endif
 }
 // Staged-heading record (multi-lane segments): the 11 QCP::inner_product terms of one heading
 // pair, as floats -- wc1_a * c2_b (a, b = x, y, z), dot(wc1, c1), dot(c2, c2).
@@ -1269,23 +1360,24 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 	LV L;
 	FP G;
 	const size_t loc0 = (s / kLocTile) * (size_t)(12 * kLocTile) * B + (s % kLocTile) * 4;
-	if constexpr (PL == 2) L.p = BPtr<float>{buf_rsrc(t.Lg, t.lg_bytes), (uint32_t)(loc0 * sizeof(float))};
+	if constexpr (PL == 2) L.p = bptr<float>(t.Lg, t.lg_bytes, (uint32_t)(loc0 * sizeof(float)), 0u, t.lg_bytes);
 	else if constexpr (PL == 1) L.p = t.Lg + loc0;
 	if constexpr (PL == 2) {
-		G = BPtr<float>{buf_rsrc(t.Sg, t.sg_bytes), (uint32_t)(s * (size_t)t.state_stride * sizeof(float))};
+		const uint32_t sb = (uint32_t)(s * (size_t)t.state_stride * sizeof(float));
+		G = bptr<float>(t.Sg, t.sg_bytes, sb, sb, sb + (uint32_t)(t.state_stride * sizeof(float)));
 	} else if constexpr (PL == 1) {
 		G = lds + (size_t)g * t.lds_stride;
 	} else {
 		L.p = lds + (size_t)g * t.lds_stride;
 		G = L.p + 12 * B;
 	}
-	const FP TG = G + 12 * t.n_gck;
-	const FP ST = TG + 12 * P;
-	const FP HS = ST + 12 * P;                        // staged headings (t.seg_hbase), 16-B aligned
-	const IP SF = rebind<int>(HS + t.hs_floats);
+	const FP TG = uplus(G, 12 * t.n_gck, 1);
+	const FP ST = uplus(TG, 12 * P, 2);
+	const FP HS = uplus(ST, 12 * P, 4);               // staged headings (t.seg_hbase), 16-B aligned
+	const IP SF = rebind<int>(uplus(HS, t.hs_floats, 8));
 	constexpr int TA = PL == 2 ? kTabTiled : (T32 ? kTab32 : kTab64); // placement 2 reads the tiled table copy
-	const FP OE = rebind<float>(SF + P);              // stabilization only: 3 per pin
-	const FP MS = OE + 3 * P;                        // stabilization only: 7 per pin
+	const FP OE = rebind<float>(uplus(SF, P, 16));    // stabilization only: 3 per pin
+	const FP MS = uplus(OE, 3 * P, 32);              // stabilization only: 7 per pin
 	if (valid) {
 		for (int b = role; b < B; b += K)
 			if (t.bone_flags[b] & mbik::BF_IN_LIST) L.st(b, pose_to_xform(pose_in + ((size_t)local * B + b) * 10));
@@ -1517,6 +1609,10 @@ struct mbik_plan {
 	float *d_Dt = nullptr, *d_CFt = nullptr;
 	double *d_CDt = nullptr;
 	int tables_version = 1, tiled_version = 0;
+	// the tiling's completion, for launches on another stream than the one that tiled
+	hipEvent_t tile_ev = nullptr;
+	hipStream_t tile_stream = nullptr;
+	bool tile_pending = false;
 };
 
 namespace {
@@ -1783,8 +1879,13 @@ int ensure_tiled_rows(mbik_plan *p, hipStream_t stream) {
 		// padding skeletons read zeros
 		if (hipMemsetAsync(a, 0, std::max<size_t>(nD, 1) * sizeof(float), stream) != hipSuccess ||
 				hipMemsetAsync(b, 0, std::max<size_t>(nCF, 1) * sizeof(float), stream) != hipSuccess ||
-				hipMemsetAsync(c, 0, std::max<size_t>(nCD, 1) * sizeof(double), stream) != hipSuccess)
+				hipMemsetAsync(c, 0, std::max<size_t>(nCD, 1) * sizeof(double), stream) != hipSuccess) {
+			(void)hipStreamSynchronize(stream);
+			(void)hipFree(a);
+			(void)hipFree(b);
+			(void)hipFree(c);
 			return fail(MBIK_EHIP, "hipMemsetAsync tiled setup tables");
+		}
 		p->d_Dt = static_cast<float *>(a);
 		p->d_CFt = static_cast<float *>(b);
 		p->d_CDt = static_cast<double *>(c);
@@ -1803,7 +1904,27 @@ int ensure_tiled_rows(mbik_plan *p, hipStream_t stream) {
 				h.cd_stride(), h.N, Npad);
 	hipError_t e = hipGetLastError();
 	if (e != hipSuccess) return fail(MBIK_EHIP, std::string("tile launch failed: ") + hipGetErrorString(e));
+	// A launch on another stream must not read the copy before the tiling has run: record its
+	// completion; launch() makes other streams wait on it until it has completed.
+	if (!p->tile_ev && hipEventCreateWithFlags(&p->tile_ev, hipEventDisableTiming) != hipSuccess) {
+		p->tile_ev = nullptr;
+		return fail(MBIK_EHIP, "hipEventCreate");
+	}
+	if (hipEventRecord(p->tile_ev, stream) != hipSuccess) return fail(MBIK_EHIP, "hipEventRecord");
+	p->tile_stream = stream;
+	p->tile_pending = true;
 	p->tiled_version = p->tables_version;
+	return MBIK_OK;
+}
+// Orders a launch on `stream` after the last tiling of the plan's tables (ensure_tiled_rows).
+int wait_tiled_rows(mbik_plan *p, hipStream_t stream) {
+	if (!p->tile_pending) return MBIK_OK;
+	if (hipEventQuery(p->tile_ev) == hipSuccess) {
+		p->tile_pending = false;
+		return MBIK_OK;
+	}
+	if (stream != p->tile_stream && hipStreamWaitEvent(stream, p->tile_ev, 0) != hipSuccess)
+		return fail(MBIK_EHIP, "hipStreamWaitEvent");
 	return MBIK_OK;
 }
 
@@ -1849,6 +1970,7 @@ int launch(mbik_plan *p, int first, int count, const float *pose_in, const float
 	DevPlan d = p->dev;
 	if (h.state_hbm == 2) {
 		if ((rc = ensure_tiled_rows(p, stream)) != MBIK_OK) return rc;
+		if ((rc = wait_tiled_rows(p, stream)) != MBIK_OK) return rc;
 		d.D = p->d_Dt;
 		d.CF = p->d_CFt;
 		d.CD = p->d_CDt;
@@ -1917,7 +2039,7 @@ void keep_inputs(mbik_plan *p, const mbik_skeleton_desc &desc, const mbik_config
 	p->src_parents.assign(desc.parents, desc.parents + (desc.parents ? desc.bone_count : 0));
 	p->src_pins.assign(desc.pins, desc.pins + (desc.pins ? desc.pin_count : 0));
 	p->src_cons.assign(desc.constraints, desc.constraints + (desc.constraints ? desc.constraint_count : 0));
-	p->src_bone_damp.assign(cfg.bone_damp, cfg.bone_damp + (cfg.bone_damp ? cfg.bone_damp_count : 0));
+	p->src_bone_damp.assign(cfg.bone_damp, cfg.bone_damp + (cfg.bone_damp ? std::max(0, cfg.bone_damp_count) : 0));
 	p->src_max_cones = desc.max_cones;
 	p->src_cfg = cfg;
 	p->src_cfg.bone_damp = nullptr;
@@ -2026,6 +2148,7 @@ int build_topologies(int n, const mbik_skeleton_desc *descs, const mbik_config *
 		else if (d.pin_count < 0 || (d.pin_count > 0 && !d.pins)) errs[i] = "invalid pins";
 		else if (d.constraint_count < 0 || (d.constraint_count > 0 && !d.constraints)) errs[i] = "invalid constraints";
 		else if (c.iterations_per_frame < 0) errs[i] = "iterations_per_frame must be >= 0";
+		else if (c.bone_damp_count < 0) errs[i] = "negative count"; // (keep_inputs would read a reversed range)
 		ok[i] = errs[i].empty();
 		const int B = ok[i] ? d.bone_count : 1, P = ok[i] ? d.pin_count : 0, C = ok[i] ? d.constraint_count : 0;
 		sz[i] = mbik::topo_sizes(B, P, C);
@@ -2197,6 +2320,14 @@ int32_t mbik_plan_create_device(int32_t n_rigs, const mbik_skeleton_desc *descs,
 	if (rc) return rc;
 	for (int i = 0; i < n_rigs; i++)
 		if (!errs[i].empty()) return fail(MBIK_EINVAL, "rig " + std::to_string(i) + ": " + errs[i]);
+	// every rig's remaining argument checks before any plan takes device memory
+	for (int i = 0; i < n_rigs; i++) {
+		for (int c : built[i].cons_order_ncones)
+			if (c > std::max(1, descs[i].max_cones))
+				return fail(MBIK_EINVAL, "rig " + std::to_string(i) + ": a constraint has more cones than max_cones");
+		if (built[i].NC > 0 && (!cones || !twist || !cones[i] || !twist[i]))
+			return fail(MBIK_EINVAL, "rig " + std::to_string(i) + ": cones/twist required when constraints exist");
+	}
 	std::vector<std::unique_ptr<mbik_plan>> plans;
 	for (int i = 0; i < n_rigs && rc == MBIK_OK; i++) {
 		const mbik_skeleton_desc &d = descs[i];
@@ -2206,10 +2337,6 @@ int32_t mbik_plan_create_device(int32_t n_rigs, const mbik_skeleton_desc *descs,
 		keep_inputs(p.get(), d, configs[i]);
 		mbik::HostPlan &h = p->host;
 		h = std::move(built[i]);
-		for (int c : h.cons_order_ncones)
-			if (c > std::max(1, d.max_cones)) return fail(MBIK_EINVAL, "a constraint has more cones than max_cones");
-		if (h.NC > 0 && (!cones || !twist || !cones[i] || !twist[i]))
-			return fail(MBIK_EINVAL, "cones/twist required when constraints exist");
 		h.N = n_skeletons[i];
 		const size_t N = (size_t)h.N;
 		h.D.assign((size_t)h.B * 9 * N, 0.0f); // filled on the device below (mbik_setup_kernel)
@@ -2217,9 +2344,10 @@ int32_t mbik_plan_create_device(int32_t n_rigs, const mbik_skeleton_desc *descs,
 		h.CD.assign((size_t)h.NC * h.cd_stride() * N, 0.0);
 		mbik::setup_tables(h);
 		h.setup_max_cones = std::max(1, d.max_cones);
-		if ((rc = finish_plan(p.get(), setup_pose[i], nullptr)) != MBIK_OK) break;
-		rc = mbik_plan_rebuild_setup(p.get(), 0, h.N, setup_pose[i], h.NC ? cones[i] : nullptr, h.NC ? twist[i] : nullptr, nullptr);
-		plans.push_back(std::move(p));
+		rc = finish_plan(p.get(), setup_pose[i], nullptr); // (frees what it took when it fails)
+		if (rc == MBIK_OK)
+			rc = mbik_plan_rebuild_setup(p.get(), 0, h.N, setup_pose[i], h.NC ? cones[i] : nullptr, h.NC ? twist[i] : nullptr, nullptr);
+		plans.push_back(std::move(p)); // released through mbik_plan_destroy below on any failure
 	}
 	if (rc) {
 		for (auto &p : plans) mbik_plan_destroy(p.release());
@@ -2233,7 +2361,7 @@ int32_t mbik_plan_create_device(int32_t n_rigs, const mbik_skeleton_desc *descs,
 // ---- plan serialisation (mbik_plan_save / mbik_plan_load) ----
 namespace {
 constexpr char kPlanMagic[8] = {'M', 'B', 'I', 'K', 'P', 'L', 'A', 'N'};
-constexpr uint32_t kPlanFormat = 1;
+constexpr uint32_t kPlanFormat = 2; // 2: the table-addressing override joins the layout overrides (1 is still read)
 struct PlanWriter {
 	std::vector<char> b;
 	void bytes(const void *v, size_t n) {
@@ -2315,7 +2443,7 @@ int32_t mbik_plan_save(const mbik_plan *p, void *buf, uint64_t capacity, uint64_
 	w.vec(CF);
 	w.vec(CD);
 	for (int32_t v : {p->lanes_override, p->spw_override, p->interval_override, p->staging_override, p->locals_override,
-				 p->waves_override, p->cm_lanes})
+				 p->waves_override, p->cm_lanes, p->tab64})
 		w.put<int32_t>(v);
 	std::vector<char> cm;
 	if (h.constraint_mode && N) {
@@ -2344,7 +2472,7 @@ int32_t mbik_plan_load(const void *buf, uint64_t size, int32_t device, mbik_plan
 	if (!r.bytes(magic, 8) || std::memcmp(magic, kPlanMagic, 8) != 0) return fail(MBIK_EINVAL, "not a saved mbik plan");
 	const uint32_t format = r.get<uint32_t>();
 	if (!r.ok) return fail(MBIK_EINVAL, "truncated or corrupt saved plan");
-	if (format != kPlanFormat) return fail(MBIK_EUNSUPPORTED, "saved plan format version not supported");
+	if (format != kPlanFormat && format != 1) return fail(MBIK_EUNSUPPORTED, "saved plan format version not supported");
 	(void)r.get<uint32_t>(); // the ABI version that wrote it (informational)
 	const int32_t N = r.get<int32_t>();
 	constexpr uint64_t kMax = 1ull << 34;
@@ -2362,8 +2490,8 @@ int32_t mbik_plan_load(const void *buf, uint64_t size, int32_t device, mbik_plan
 	const int32_t setup_max_cones = r.get<int32_t>();
 	std::vector<float> D = r.vec<float>(kMax), CF = r.vec<float>(kMax);
 	std::vector<double> CD = r.vec<double>(kMax);
-	int32_t ov[7];
-	for (int32_t &v : ov) v = r.get<int32_t>();
+	int32_t ov[8] = {};
+	for (int i = 0; i < (format >= 2 ? 8 : 7); i++) ov[i] = r.get<int32_t>();
 	std::vector<char> cm = r.vec<char>(kMax);
 	if (!r.ok || N <= 0) return fail(MBIK_EINVAL, "truncated or corrupt saved plan");
 	mbik_skeleton_desc desc{};
@@ -2398,6 +2526,7 @@ int32_t mbik_plan_load(const void *buf, uint64_t size, int32_t device, mbik_plan
 	p->locals_override = ov[4];
 	p->waves_override = ov[5];
 	p->cm_lanes = ov[6];
+	p->tab64 = ov[7] != 0;
 	if (h.constraint_mode) {
 		const int W = std::max(1, (h.cm_npos + 31) / 32);
 		const size_t want = (size_t)(3 * h.B + 2 * h.NC) * 12 * n * sizeof(float) + 4 * (size_t)W * n * sizeof(uint32_t);
@@ -2418,6 +2547,7 @@ void mbik_plan_destroy(mbik_plan *p) {
 	if (p->d_in) (void)hipFree(p->d_in);
 	if (p->d_tg) (void)hipFree(p->d_tg);
 	if (p->d_out) (void)hipFree(p->d_out);
+	if (p->tile_ev) (void)hipEventDestroy(p->tile_ev);
 	delete p;
 }
 

@@ -243,11 +243,16 @@ def test_waves_argument_check(mbik):
         plan.set_waves_per_simd(3)
 
 
-@pytest.mark.parametrize("cfg,n,pin", [(3, 65536, None), (5, 16384, (8, 8, 1, 0, 2, 2))])
+@pytest.mark.parametrize("cfg,n,pin", [(3, 65536, None), (5, 16384, (8, 8, 1, 0, 2, 2)), (4, 32768, None),
+                                       (4, 262144, (4, 16, 1, 0, 2, 2))])
 def test_tuned_full_size_layouts_are_exact(oracle, mbik, cfg, n, pin):
-    """Full-size launches on the layouts autotune picks for them (C3: autotuned here; C5: the
-    layout its autotune picks, pinned -- 8 lanes x 8, unstaged, all state in device memory, two
-    waves per SIMD); oracle spot checks at the start, middle and end of the batch."""
+    """Full-size launches on the layouts autotune picks for them (C3, and C4 at its 32,768
+    skeletons per GPU: autotuned here; C5: the layout its autotune picks, pinned -- 8 lanes x 8,
+    unstaged, all state in device memory, two waves per SIMD; C4's whole 262,144-skeleton batch
+    of BASELINE configs[3] on one GPU: the strong-scaling layout, pinned -- 4 lanes x 16, all
+    state in device memory (each area < 4 GiB: the buffer-resource guard), two waves per SIMD); oracle
+    spot checks at the start, middle and end of the batch.  C4 is the multi-segment branching
+    rig of ik_bone_segment_3d.cpp:210-225 (11 segments, post-order recursion)."""
     import torch
     wl = W.generate(cfg, n)
     plan = Plan.from_workload(wl)
@@ -268,7 +273,14 @@ def test_tuned_full_size_layouts_are_exact(oracle, mbik, cfg, n, pin):
     torch.cuda.synchronize()
     got = po.cpu().numpy()
     info = plan.info()
-    for first in (0, n // 2 - 3, n - 6):
+    if pin is not None:
+        assert (info["lanes_per_skeleton"], info["state_placement"], info["waves_per_simd"]) == (pin[0], pin[4], pin[5])
+    # whole batch: finite, unit rotations (size-independent properties)
+    assert np.isfinite(got).all(), f"C{cfg} x {n}: non-finite output"
+    qn = np.linalg.norm(got[..., :4].astype(np.float64), axis=-1)
+    assert np.abs(qn - 1.0).max() < 1e-5, f"C{cfg} x {n}: non-unit rotation"
+    spots = (0, n // 2 - 3, n - 6) if n <= 65536 else (0, n // 3 + 1, n // 2 - 3, 2 * n // 3 + 5, n - 22, n - 6)
+    for first in spots:
         sub = W.generate(cfg, 6, first=first)
         ref = oracle.Oracle(sub).solve(sub.pose, sub.targets, threads=8)
         assert_parity(got[first:first + 6], ref, f"C{cfg} tuned layout {info} @{first}")

@@ -33,6 +33,24 @@ def test_loaded_plan_solves_bitwise(oracle, mbik, cfg, n):
     assert b.save() == data
 
 
+def test_table_addressing_override_survives(oracle, mbik):
+    """mbik_plan_set_table_addressing(1) is one of the saved layout overrides (format 2): the
+    loaded plan still runs the 64-bit-index kernel -- bitwise like the original -- and so still
+    refuses placement 1, which needs the 32-bit form."""
+    wl = W.generate(2, 24, first=11)
+    a = Plan.from_workload(wl)
+    a.set_table_addressing(1)
+    data = a.save()
+    b = Plan.load(data)
+    assert b.save() == data
+    got = b.solve_host(wl.pose, wl.targets)
+    assert np.array_equal(got.view(np.uint32), a.solve_host(wl.pose, wl.targets).view(np.uint32))
+    assert_parity(got, oracle.Oracle(wl).solve(wl.pose, wl.targets, threads=8), "loaded 64-bit-table plan")
+    b.set_locals_placement(1)
+    with pytest.raises(_lib.MbikError):
+        b.solve_host(wl.pose, wl.targets)
+
+
 def test_rebuilt_setup_tables_survive(mbik):
     import torch
     wl = W.generate(5, 6)

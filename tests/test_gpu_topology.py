@@ -80,6 +80,29 @@ def test_device_plans_refuse_bad_rigs(mbik):
     assert e.value.code == _lib.MBIK_EINVAL and "cycle" in str(e.value)
 
 
+def test_device_plans_bad_rig_after_good_leaks_nothing(mbik):
+    """A crowd whose second rig is refused (more cones than max_cones) fails as a whole, before
+    the first rig's plan takes device memory: repeating the call frees as much as it took."""
+    import torch
+    from many_bone_ik_amd import _lib
+    dev = torch.device("cuda", 0)
+    wl = W.generate(5, 2048)                       # ~130 MB of setup tables per good plan
+    keep = [torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in (wl.pose, wl.cones, wl.twist)]
+    bad_pose = torch.zeros((1, 2, 10), device=dev)
+    bad_cones = torch.zeros((1, 1, 3, 4), device=dev)
+    bad_twist = torch.zeros((1, 1, 3), device=dev)
+    bad = (np.array([-1, 0], np.int32), [dict(bone=1)], [dict(bone=1, cone_count=3)], {"max_cones": 1})
+    torch.cuda.synchronize()
+    free0 = torch.cuda.mem_get_info(0)[0]
+    for _ in range(4):
+        with pytest.raises(_lib.MbikError) as e:
+            plans_from_device([rig_of_workload(wl), bad], [wl.n, 1], [keep[0].data_ptr(), bad_pose.data_ptr()],
+                              [keep[1].data_ptr(), bad_cones.data_ptr()], [keep[2].data_ptr(), bad_twist.data_ptr()])
+        assert e.value.code == _lib.MBIK_EINVAL and "rig 1" in str(e.value)
+    torch.cuda.synchronize()
+    assert torch.cuda.mem_get_info(0)[0] >= free0 - (64 << 20)
+
+
 def test_device_builder_on_a_large_random_crowd(mbik):
     """2,048 random rigs (random trees, pins, priorities, weights, propagation factors,
     constraints, damping, stabilization) built in one launch: every table as the host's."""

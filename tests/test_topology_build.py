@@ -74,3 +74,21 @@ def test_topo_builder_equals_host_builder():
     mism, err = topology_selftest(rigs, device=-1)
     bad = [i for i, m in enumerate(mism) if m]
     assert not bad, f"rigs {bad[:10]} differ: {err}"
+
+
+def test_negative_bone_damp_count_is_refused_by_both_builders():
+    """A negative bone_damp_count is refused with the same message by the host builder
+    (mbik_plan_create / mbik_describe_topology) and the device-side one (build_topologies:
+    mbik_plan_create_device would otherwise copy a reversed range)."""
+    import ctypes as C
+    from many_bone_ik_amd import _lib
+    from many_bone_ik_amd.solver import _rig_arrays
+    L = _lib.load()
+    rigs = [rig([-1, 0, 1], [2], [], 0, bone_damp=np.full(3, 0.1, np.float32))] * 2
+    descs, cfgs, keep = _rig_arrays(rigs)
+    cfgs[1].bone_damp_count = -1
+    assert L.mbik_describe_topology(C.byref(descs[1]), C.byref(cfgs[1]), None, None, None, None, None, None) == _lib.MBIK_EINVAL
+    assert "negative count" in _lib.last_error()
+    out = (C.c_int32 * 2)()
+    assert L.mbik_selftest_topology(2, descs, cfgs, -1, out) == 0
+    assert list(out) == [0, 0], _lib.last_error()
