@@ -155,7 +155,6 @@ def main():
     dev = torch.device("cuda", local_rank)
 
     from many_bone_ik_amd import workloads as W
-    from many_bone_ik_amd.dist import gather_poses, gather_poses_to_root
     from many_bone_ik_amd.solver import Plan, quat_error
 
     cfg = args.config
@@ -209,29 +208,9 @@ def main():
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     wall_max = float(elapsed.item())
 
-    gather_ms = gather_root_ms = None
+    gather = None
     if dist:
-        dist.barrier()
-        torch.cuda.synchronize(dev)
-        g0 = time.perf_counter()
-        gather_poses(pose_out, total)
-        torch.cuda.synchronize(dev)
-        gt = torch.tensor([time.perf_counter() - g0], dtype=torch.float64, device=dev)
-        dist.all_reduce(gt, op=dist.ReduceOp.MAX)
-        gather_ms = float(gt.item()) * 1e3
-        # SURVEY §8(e)'s variant: every rank sends its shard to rank 0 only (one xGMI link
-        # each).  Reported beside the solve, never part of `value`; a failure is reported too.
-        try:
-            dist.barrier()
-            torch.cuda.synchronize(dev)
-            g0 = time.perf_counter()
-            gather_poses_to_root(pose_out, total, root=0)
-            torch.cuda.synchronize(dev)
-            gt = torch.tensor([time.perf_counter() - g0], dtype=torch.float64, device=dev)
-            dist.all_reduce(gt, op=dist.ReduceOp.MAX)
-            gather_root_ms = float(gt.item()) * 1e3
-        except Exception as e:  # noqa: BLE001 -- measurement only
-            gather_root_ms = f"error: {e}"
+        gather = timed_gathers(pose_out, total, dist, lambda: torch.cuda.synchronize(dev), torch.device(dev))
 
     # PCIe-inclusive rate (host buffers in, solve, host buffers out): reported, never `value`
     pcie = None
@@ -333,8 +312,9 @@ def main():
                  "algorithmic_flops_per_launch": alg_flops,
                  "note": "SURVEY.md §8(d) flop formula; the bound that applies to this path (DESIGN.md §5)"},
         "issue": issue,
-        "gather_ms": gather_ms,
-        "gather_to_root_ms": gather_root_ms,
+        "gather_ms": gather["all_gather"]["ms"] if gather else None,
+        "gather_to_root_ms": gather["to_root"].get("ms", gather["to_root"].get("error")) if gather else None,
+        "gather": gather,
         "pcie_inclusive": pcie,
         "parity": parity,
     }
@@ -352,6 +332,44 @@ def layout_key(info: dict) -> str:
     """The launch layout a plan runs (mbik_plan_info), as the suffix of profiles/traffic.json keys."""
     return (f"K{info['lanes_per_skeleton']}_s{info['skeletons_per_block']}_i{info['checkpoint_interval']}"
             f"_st{info['heading_staging']}_pl{info['state_placement']}_w{info['waves_per_simd']}")
+
+
+def timed_gathers(pose_out, total: int, dist, sync, dev) -> dict:
+    """Times SURVEY §8(e)'s final gather of the output poses two ways, after the solve loop and
+    outside `value`, and reports what each moves: `all_gather` (RCCL all_gather: every rank gets
+    every pose) and `to_root` (dist.gather: each peer sends its shard to rank 0 over its own
+    xGMI link).  Shards are padded to the largest for one fixed-size collective, so the bytes
+    below are the padded messages.  ms = max over ranks; GB/s = bytes received by the busiest
+    receiver / ms."""
+    import torch
+    from many_bone_ik_amd.dist import gather_poses, gather_poses_to_root, shard_range
+    world = dist.get_world_size()
+    per_skel = int(pose_out[0].numel() * pose_out.element_size()) if pose_out.shape[0] else 0
+    cmax = max(shard_range(r, world, total)[1] for r in range(world))
+    msg = cmax * per_skel                 # one rank's (padded) shard
+    recv = (world - 1) * msg              # what the busiest receiver takes in
+
+    def timed(fn):
+        dist.barrier()
+        sync()
+        g0 = time.perf_counter()
+        fn()
+        sync()
+        gt = torch.tensor([time.perf_counter() - g0], dtype=torch.float64, device=dev)
+        dist.all_reduce(gt, op=dist.ReduceOp.MAX)
+        return float(gt.item()) * 1e3
+
+    out = {"pose_bytes_total": total * per_skel, "shard_bytes_padded": msg}
+    ms = timed(lambda: gather_poses(pose_out, total))
+    out["all_gather"] = {"ms": ms, "bytes_in_per_rank": recv, "bytes_out_per_rank": msg,
+                         "GBps_in_per_rank": recv / (ms * 1e-3) / 1e9 if ms > 0 else None}
+    try:
+        ms = timed(lambda: gather_poses_to_root(pose_out, total, root=0))
+        out["to_root"] = {"ms": ms, "bytes_in_root": recv, "bytes_out_per_peer": msg,
+                          "GBps_in_root": recv / (ms * 1e-3) / 1e9 if ms > 0 else None}
+    except Exception as e:  # noqa: BLE001 -- measurement only: reported, never part of `value`
+        out["to_root"] = {"error": str(e)}
+    return out
 
 
 def batch_shard(args, world: int, rank: int):
@@ -387,11 +405,12 @@ def dry_run(args, world: int, rank: int):
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     full = gather_poses(shard, total) if world > 1 else shard
     ok = bool(torch.equal(full[:, 0, 0], torch.arange(total, dtype=torch.float32)))
+    gather = timed_gathers(shard, total, dist, lambda: None, torch.device("cpu")) if world > 1 else None
     if rank == 0:
         print(json.dumps({"metric": METRIC, "value": None, "unit": "skeletons/s", "n_gpus": world,
                           "steps": args.steps, "warmup": args.warmup, "scaling": args.scaling, "dry_run": True,
                           "config": {"skeletons_total": total, "skeletons_per_gpu": n},
-                          "gathered_in_order": ok, "max_wall_s": float(el.item())}))
+                          "gathered_in_order": ok, "max_wall_s": float(el.item()), "gather": gather}))
     if world > 1:
         dist.destroy_process_group()
 

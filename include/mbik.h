@@ -101,7 +101,7 @@ typedef struct mbik_plan_info {
 	int32_t max_headings;
 	int32_t device;
 	int64_t device_bytes;              /* per-skeleton plan tables resident in HBM */
-	double algorithmic_bytes_per_skeleton; /* pose in/out + targets + plan tables read once */
+	double algorithmic_bytes_per_skeleton; /* per bone pose in/out 80 B + bone-direction quaternion 16 B + damp 4 B; per effector 64 B; per constrained bone 52 B + 52 B per cone (C2 8,292 B) */
 	double algorithmic_flops_per_skeleton; /* SURVEY.md §8(d) per-bone-step formula x bone-steps x iterations */
 	int64_t lds_bytes_per_block;       /* LDS of one launch block (spw skeletons + topology tables) */
 	int32_t checkpoint_interval;       /* iteration-start globals kept every n-th bone (1 << 20: segment roots only) */

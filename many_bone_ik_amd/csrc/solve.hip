@@ -2088,16 +2088,6 @@ int finish_plan(mbik_plan *p, const float *setup_pose, const void *cm_state) {
 		p->d_sched = nullptr;
 		return rc;
 	}
-	// Algorithmic HBM bytes per skeleton, each byte the solve needs read once and each
-	// output written once: poses in + out, targets, the bone-direction
-	// basis of every bone whose bone-direction frame is read (effector bones and
-	// cone-constrained bones), and the constraint slots.
-	int ndir = 0;
-	for (int b = 0; b < h.B; b++) {
-		bool used = (h.bone_flags[b] & mbik::BF_ORIENT) != 0;
-		for (int e = 0; e < h.P && !used; e++) used = h.eff_bone[e] == b;
-		ndir += used;
-	}
 	// Algorithmic flops: per bone-step 50 H + 14 H [translate] + 72 E_seg
 	// + 465, plus 770 + 140 C - 60 for a constrained bone with C cones; x iterations.
 	double f = 0;
@@ -2114,8 +2104,17 @@ int finish_plan(mbik_plan *p, const float *setup_pose, const void *cm_state) {
 		}
 	}
 	p->alg_flops = f * h.iterations;
-	p->alg_bytes = (double)h.B * 10 * 4 * 2 + (double)h.P * 12 * 4 + (double)ndir * 9 * 4 +
-			(double)h.NC * ((14.0 + 13.0 * h.max_cones) * 4.0 + h.cd_stride() * 8.0); // the per-cone derived constants (CFC_NCP..) excluded
+	// Algorithmic HBM bytes per skeleton, SURVEY.md §8(d)'s definition (the one bench.py's
+	// roofline and BASELINE.md divide by): each input the solve needs read once, each output
+	// written once -- per bone the input pose (quaternion, position, scale: 40 B), its
+	// bone-direction quaternion (16 B) and damp (4 B), and the output pose (40 B); per
+	// effector the target transform (48 B) and its weight and priorities (16 B); per
+	// constrained bone the orientation and twist quaternions, the twist centre (16 B each),
+	// the twist half-cosine (4 B) and 52 B per cone.  C2 8,292 B, C3 3,456, C4 6,912,
+	// C5 52,068.
+	double cons = 0;
+	for (int c = 0; c < h.NC; c++) cons += 16.0 * 3 + 4.0 + 52.0 * h.cons_ncones[c];
+	p->alg_bytes = (double)h.B * (40 + 16 + 4 + 40) + (double)h.P * (48 + 16) + cons;
 	if (h.constraint_mode) // the persistent node caches, read and written once per frame
 		p->alg_bytes += 2.0 * ((double)(3 * h.B + 2 * h.NC) * 12 * 4 + 4.0 * p->cm.W * 4);
 	h.D.clear(); h.D.shrink_to_fit();

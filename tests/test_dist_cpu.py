@@ -80,6 +80,13 @@ def test_bench_launches_its_own_ranks(scaling, total):
     assert line["dry_run"] and line["n_gpus"] == 2 and line["scaling"] == scaling
     assert line["config"]["skeletons_total"] == total
     assert line["gathered_in_order"]
+    # the gathers report what they move: skeletons of [1, 10] floats, shards padded to the larger
+    g = line["gather"]
+    shard = (total + 1) // 2 * 10 * 4
+    assert g["pose_bytes_total"] == total * 40 and g["shard_bytes_padded"] == shard
+    assert g["all_gather"]["bytes_in_per_rank"] == shard and g["all_gather"]["ms"] > 0
+    assert g["all_gather"]["GBps_in_per_rank"] > 0
+    assert g["to_root"]["bytes_in_root"] == shard and g["to_root"]["GBps_in_root"] > 0
 
 
 def test_bench_refuses_world_mismatch():
