@@ -50,7 +50,7 @@ extern "C" {
 #define MBIK_EUNSUPPORTED (-4)
 #define MBIK_ENODEV (-5)
 
-#define MBIK_ABI_VERSION 3
+#define MBIK_ABI_VERSION 4
 
 typedef struct mbik_plan mbik_plan;
 typedef struct mbik_group mbik_group;
@@ -111,13 +111,37 @@ typedef struct mbik_plan_info {
 	int32_t constraint_slots;          /* slots of mbik_plan_setup_tables' CF / CD (ABI 3) */
 	int32_t cf_stride;                 /* floats per slot of CF = 14 + 31*max_cones (ABI 3) */
 	int32_t cd_stride;                 /* doubles per slot of CD = 2*max_cones (ABI 3) */
+	int32_t libm_variant;              /* mbik_plan_options.libm_variant the plan was created with (ABI 4) */
 } mbik_plan_info;
+
+/* Which reference host the plan reproduces bit for bit (ABI 4).  Godot's Math::sin/cos(float)
+ * call the platform ::sinf/::cosf -- glibc on the reference's Linux x86-64 build -- and glibc
+ * 2.35 ships two builds of them, picked per CPU by an ifunc; they differ on 12 (sinf) and 22
+ * (cosf) of the 2^32 float inputs, and the solve amplifies a 1-ulp difference ~2x per
+ * iteration, so the choice is part of the reference's behaviour:
+ *   MBIK_LIBM_VARIANT_FMA   (0, default) the FMA build: a reference running on any x86-64
+ *                           CPU with FMA (every Intel since Haswell, AMD since Piledriver;
+ *                           the GPU boxes' EPYC 9575F);
+ *   MBIK_LIBM_VARIANT_SSE2  (1) the SSE2 build: a reference on a CPU without FMA, or with the
+ *                           ifunc disabled (GLIBC_TUNABLES=glibc.cpu.hwcaps=-FMA,-AVX2_Usable).
+ * acosf has a single build.  The variant applies to the setup tables (cone and twist
+ * half-angle sines/cosines, tangent frames) and to the solve's slerp coefficient. */
+#define MBIK_LIBM_VARIANT_FMA 0
+#define MBIK_LIBM_VARIANT_SSE2 1
+typedef struct mbik_plan_options {
+	int32_t struct_size;               /* sizeof(mbik_plan_options): later fields are optional */
+	int32_t libm_variant;              /* MBIK_LIBM_VARIANT_* */
+} mbik_plan_options;
 
 /* Builds the per-topology tables and the per-skeleton setup data for skeletons
  * [0, n_skeletons) from their setup poses, uploads them to `device`.  cones/twist may be
  * NULL when constraint_count == 0. */
 int32_t mbik_plan_create(const mbik_skeleton_desc *desc, const mbik_config *config, int32_t n_skeletons,
 		const float *setup_pose, const float *cones, const float *twist, int32_t device, mbik_plan **out_plan);
+/* mbik_plan_create with creation options (ABI 4; opts NULL = the defaults). */
+int32_t mbik_plan_create_opts(const mbik_skeleton_desc *desc, const mbik_config *config, const mbik_plan_options *opts,
+		int32_t n_skeletons, const float *setup_pose, const float *cones, const float *twist, int32_t device,
+		mbik_plan **out_plan);
 void mbik_plan_destroy(mbik_plan *plan);
 /* Plan serialisation to a flat binary (checkpoint / resume, or a plan built once and shipped):
  * the creation inputs (topology, pins, constraints, config), the per-skeleton setup tables as
@@ -185,6 +209,10 @@ int32_t mbik_plan_rebuild_setup(mbik_plan *plan, int32_t first, int32_t count, c
 int32_t mbik_plan_create_device(int32_t n_rigs, const mbik_skeleton_desc *descs, const mbik_config *configs,
 		const int32_t *n_skeletons, const float *const *setup_pose, const float *const *cones, const float *const *twist,
 		int32_t device, mbik_plan **out_plans);
+/* mbik_plan_create_device with creation options, the same for every rig (ABI 4). */
+int32_t mbik_plan_create_device_opts(int32_t n_rigs, const mbik_skeleton_desc *descs, const mbik_config *configs,
+		const mbik_plan_options *opts, const int32_t *n_skeletons, const float *const *setup_pose, const float *const *cones,
+		const float *const *twist, int32_t device, mbik_plan **out_plans);
 /* Self-test of the GPU topology build: builds the n rigs with topo.h on `device` (or on the
  * host when device < 0: the same code) and compares every topology table with the host
  * builder's (mbik_plan_create's).  mismatches[i] = number of differing tables of rig i (0 when
@@ -319,13 +347,19 @@ int32_t mbik_selftest_div(int32_t device, uint64_t random_iterations, uint64_t o
  *   SLERP_SCALE0         (float)(sin((double)w) / (double)sinf(w)): Quaternion::slerp's
  *                        weight-0 coefficient (ik_bone_segment_3d.cpp:148-151)
  *   COS_F64_OF_F32       cos((double)x): a cone radius cosine (ik_open_cone_3d.h:47-56)
- *   COS_F64              cos(x): tangent-radius cosines (ik_open_cone_3d.cpp:36-120) */
+ *   COS_F64              cos(x): tangent-radius cosines (ik_open_cone_3d.cpp:36-120)
+ *   SINF_SSE2, COSF_SSE2, SLERP_SCALE0_SSE2   the same for a plan created with
+ *                        libm_variant = MBIK_LIBM_VARIANT_SSE2 (compare with a host libm
+ *                        whose FMA ifunc is disabled: GLIBC_TUNABLES=glibc.cpu.hwcaps=-FMA,-AVX2_Usable) */
 #define MBIK_LIBM_SINF 0
 #define MBIK_LIBM_COSF 1
 #define MBIK_LIBM_ACOSF 2
 #define MBIK_LIBM_SLERP_SCALE0 3
 #define MBIK_LIBM_COS_F64_OF_F32 4
 #define MBIK_LIBM_COS_F64 5
+#define MBIK_LIBM_SINF_SSE2 6
+#define MBIK_LIBM_COSF_SSE2 7
+#define MBIK_LIBM_SLERP_SCALE0_SSE2 8
 int32_t mbik_selftest_libm(int32_t fn, uint64_t first, uint64_t count, const double *inputs, const void *expected,
 		uint64_t out[3], void *hip_stream);
 

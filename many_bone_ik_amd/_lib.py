@@ -19,10 +19,15 @@ MBIK_EUNSUPPORTED = -4
 MBIK_ENODEV = -5
 
 # mbik_selftest_libm function codes (include/mbik.h)
-LIBM_SINF, LIBM_COSF, LIBM_ACOSF, LIBM_SLERP_SCALE0, LIBM_COS_F64_OF_F32, LIBM_COS_F64 = range(6)
+LIBM_SINF, LIBM_COSF, LIBM_ACOSF, LIBM_SLERP_SCALE0, LIBM_COS_F64_OF_F32, LIBM_COS_F64, LIBM_SINF_SSE2, LIBM_COSF_SSE2, \
+    LIBM_SLERP_SCALE0_SSE2 = range(9)
+# mbik_plan_options.libm_variant: the reference host's glibc sinf/cosf build
+LIBM_VARIANT_FMA, LIBM_VARIANT_SSE2 = 0, 1
+# a process's environment that makes ITS glibc pick the SSE2 build (the reference host of LIBM_VARIANT_SSE2)
+GLIBC_SSE2_TUNABLES = "glibc.cpu.hwcaps=-FMA,-AVX2_Usable"
 
 EXPORTED_SYMBOLS = (
-    "mbik_plan_create", "mbik_plan_destroy", "mbik_plan_save", "mbik_plan_load", "mbik_plan_get_info", "mbik_plan_set_launch", "mbik_plan_set_layout",
+    "mbik_plan_create", "mbik_plan_create_opts", "mbik_plan_create_device_opts", "mbik_plan_destroy", "mbik_plan_save", "mbik_plan_load", "mbik_plan_get_info", "mbik_plan_set_launch", "mbik_plan_set_layout",
     "mbik_plan_autotune", "mbik_plan_resident_blocks", "mbik_plan_set_heading_staging",
     "mbik_plan_set_locals_placement", "mbik_plan_set_waves_per_simd", "mbik_plan_set_table_addressing", "mbik_plan_rebuild_setup", "mbik_plan_setup_tables",
     "mbik_solve", "mbik_solve_checked", "mbik_solve_host", "mbik_segment_solve", "mbik_plan_segment_table", "mbik_describe_topology",
@@ -62,7 +67,11 @@ class MbikPlanInfo(C.Structure):
                 ("algorithmic_flops_per_skeleton", C.c_double), ("lds_bytes_per_block", C.c_int64),
                 ("checkpoint_interval", C.c_int32), ("heading_staging", C.c_int32), ("state_placement", C.c_int32),
                 ("waves_per_simd", C.c_int32), ("constraint_slots", C.c_int32), ("cf_stride", C.c_int32),
-                ("cd_stride", C.c_int32)]
+                ("cd_stride", C.c_int32), ("libm_variant", C.c_int32)]
+
+
+class MbikPlanOptions(C.Structure):
+    _fields_ = [("struct_size", C.c_int32), ("libm_variant", C.c_int32)]
 
 
 class MbikError(RuntimeError):
@@ -94,6 +103,12 @@ def load():
     L.mbik_plan_create.argtypes = [C.POINTER(MbikSkeletonDesc), C.POINTER(MbikConfig), C.c_int32, vp, vp, vp, C.c_int32,
                                    C.POINTER(vp)]
     L.mbik_plan_create.restype = C.c_int32
+    L.mbik_plan_create_opts.argtypes = [C.POINTER(MbikSkeletonDesc), C.POINTER(MbikConfig), C.POINTER(MbikPlanOptions), C.c_int32,
+                                        vp, vp, vp, C.c_int32, C.POINTER(vp)]
+    L.mbik_plan_create_opts.restype = C.c_int32
+    L.mbik_plan_create_device_opts.argtypes = [C.c_int32, vp, vp, C.POINTER(MbikPlanOptions), C.POINTER(C.c_int32),
+                                               C.POINTER(vp), C.POINTER(vp), C.POINTER(vp), C.c_int32, C.POINTER(vp)]
+    L.mbik_plan_create_device_opts.restype = C.c_int32
     L.mbik_plan_destroy.argtypes = [vp]
     L.mbik_plan_destroy.restype = None
     L.mbik_plan_save.argtypes = [vp, vp, C.c_uint64, C.POINTER(C.c_uint64)]

@@ -146,22 +146,32 @@ constexpr double kHalfPi = 0x1.921FB54442D18p0;
 constexpr double kC0 = 0x1p0, kC1 = -0x1.ffffffd0c621cp-2, kC2 = 0x1.55553e1068f19p-5, kC3 = -0x1.6c087e89a359dp-10,
 				 kC4 = 0x1.99343027bf8c3p-16;
 constexpr double kS1 = -0x1.555545995a603p-3, kS2 = 0x1.1107605230bc4p-7, kS3 = -0x1.994eb3774cf24p-13;
+// a*b + c as glibc's build computes it: one fused multiply-add in the FMA ifunc variant
+// (s_sinf-fma.c, what every CPU with FMA selects), two roundings in the SSE2 variant
+// (the plain s_sinf.c build, a host without FMA or with the FMA ifunc disabled)
+template <bool FMA>
+GDI double gmadd(double a, double b, double c) {
+	if constexpr (FMA) return fma(a, b, c);
+	else return a * b + c;
+}
 // sin(x) for the reduced x, x2 = x*x (sinf_poly, even quadrant)
+template <bool FMA>
 GDI float sin_poly(double x, double x2) {
 	const double x3 = x * x2;
-	const double s1 = fma(x2, kS3, kS2);
+	const double s1 = gmadd<FMA>(x2, kS3, kS2);
 	const double x7 = x3 * x2;
-	const double s = fma(x3, kS1, x);
-	return (float)fma(x7, s1, s);
+	const double s = gmadd<FMA>(x3, kS1, x);
+	return (float)gmadd<FMA>(x7, s1, s);
 }
 // cos(x) for the reduced x (sinf_poly, odd quadrant, first table)
+template <bool FMA>
 GDI float cos_poly(double x2) {
 	const double x4 = x2 * x2;
-	const double c2 = fma(x2, kC4, kC3);
-	const double c1 = fma(x2, kC1, kC0);
+	const double c2 = gmadd<FMA>(x2, kC4, kC3);
+	const double c1 = gmadd<FMA>(x2, kC1, kC0);
 	const double x6 = x4 * x2;
-	const double c = fma(x4, kC2, c1);
-	return (float)fma(x6, c2, c);
+	const double c = gmadd<FMA>(x4, kC2, c1);
+	return (float)gmadd<FMA>(x6, c2, c);
 }
 // Payne-Hanek reduction for |y| >= 120 (reduce_large): x * 2^63 / (pi/2) from the bits of
 // 2/pi, in 64-bit integers.  Returns the reduced argument and the quadrant count.
@@ -185,19 +195,20 @@ GDI double reduce_large(uint32_t xi, int &quadrant) {
 	quadrant = (int)n;
 	return (double)(int64_t)a * 0x1.921FB54442D18p-62;
 }
-// sinf (cos_variant 0) / cosf (cos_variant 1)
+// sinf (cos_variant 0) / cosf (cos_variant 1); FMA: glibc's FMA ifunc variant, else SSE2
+template <bool FMA>
 GDI float sincosf(float y, int cos_variant) {
 	const uint32_t t = top12(y);
 	double x = y;
 	if (t < 0x3f4u) { // |y| < 0.75 (abstop12(pi/4))
 		if (t < 0x398u) return cos_variant ? 1.0f : y; // |y| < 2^-12
-		return cos_variant ? cos_poly(x * x) : sin_poly(x, x * x);
+		return cos_variant ? cos_poly<FMA>(x * x) : sin_poly<FMA>(x, x * x);
 	}
 	int n, ns; // quadrant; quadrant for the sign pattern and table (large inputs add the sign bit)
 	if (t < 0x42fu) { // |y| < 120: reduce_fast
 		const double r = x * kHalfPiInv24;
 		n = ((int32_t)r + 0x800000) >> 24;
-		x = fma(-(double)n, kHalfPi, x);
+		x = FMA ? fma(-(double)n, kHalfPi, x) : x - (double)n * kHalfPi; // x - n * hpi
 		ns = n;
 	} else if (t < 0x7f8u) {
 		union {
@@ -212,8 +223,8 @@ GDI float sincosf(float y, int cos_variant) {
 	// sign of the reduced argument (+, -, -, +) by ns, the sin or cos polynomial by n, the
 	// cosine one negated when ns is in quadrant 2 or 3 (the second table)
 	const double xs = ((ns + 1) & 2) ? -x : x;
-	if (((n ^ cos_variant) & 1) == 0) return sin_poly(xs, xs * xs);
-	const float c = cos_poly(xs * xs);
+	if (((n ^ cos_variant) & 1) == 0) return sin_poly<FMA>(xs, xs * xs);
+	const float c = cos_poly<FMA>(xs * xs);
 	return (ns & 2) ? -c : c;
 }
 // acosf (e_acosf.c)
@@ -263,8 +274,14 @@ GDI float acosf(float x) {
 }
 } // namespace glibc
 
-GDI float sin_f(float x) { return glibc::sincosf(x, 0); }
-GDI float cos_f(float x) { return glibc::sincosf(x, 1); }
+// Which glibc build the reference host's sinf/cosf are (the plan's libm_variant,
+// mbik_plan_options): LIBM_FMA (0) the FMA ifunc variant -- any x86-64 CPU with FMA, the
+// default; LIBM_SSE2 (1) the SSE2 build -- a CPU without FMA, or GLIBC_TUNABLES=
+// glibc.cpu.hwcaps=-FMA,-AVX2_Usable.  They differ on 12 (sinf) and 22 (cosf) of the 2^32
+// inputs; acosf has one build.
+constexpr int LIBM_FMA = 0, LIBM_SSE2 = 1;
+GDI float sin_f(float x, int lv = LIBM_FMA) { return lv == LIBM_SSE2 ? glibc::sincosf<false>(x, 0) : glibc::sincosf<true>(x, 0); }
+GDI float cos_f(float x, int lv = LIBM_FMA) { return lv == LIBM_SSE2 ? glibc::sincosf<false>(x, 1) : glibc::sincosf<true>(x, 1); }
 GDI float acos_f(float x) { return glibc::acosf(x); }
 // Quaternion::slerp's coefficient of the start quaternion at weight 0 (Godot 4.3
 // quaternion.cpp, reached from Basis::slerp at ik_bone_segment_3d.cpp:148-151):
@@ -296,8 +313,8 @@ GDI double sin_taylor(double x) {
 	p = fma(p, x2, -0x1.5555555555555p-3);   // -1/3!
 	return fma(x * x2, p, x);
 }
-GDI float slerp_scale0(float omega) {
-	const float sinom = sin_f(omega);
+GDI float slerp_scale0(float omega, int lv = LIBM_FMA) {
+	const float sinom = sin_f(omega, lv);
 	if (fabsf(omega) <= 1.6f) {
 		const double q = sin_taylor((double)omega) * gd_rcp(sinom).r;
 		const double w = fabs(q) * 0x1p-46;
@@ -307,8 +324,8 @@ GDI float slerp_scale0(float omega) {
 	return (float)(sin((double)omega) / (double)sinom);
 }
 #else
-GDI float slerp_scale0(float omega) {
-	const float sinom = sin_f(omega);
+GDI float slerp_scale0(float omega, int lv = LIBM_FMA) {
+	const float sinom = sin_f(omega, lv);
 	return (float)(sin((double)omega) / (double)sinom);
 }
 #endif
@@ -434,18 +451,18 @@ GDI V3 xform(Q q, V3 v) {
 	return v + ((uv * q.w) + cross(u, uv)) * 2.0f;
 }
 // Quaternion(axis, angle): s = sin(a/2) / |axis|
-GDI Q axis_angle(V3 axis, float angle) {
+GDI Q axis_angle(V3 axis, float angle, int lv = LIBM_FMA) {
 	float d = length(axis);
 	if (d == 0) return q4(0, 0, 0, 0);
-	float s = sin_f(angle * 0.5f) / d;
-	return q4(axis.x * s, axis.y * s, axis.z * s, cos_f(angle * 0.5f));
+	float s = sin_f(angle * 0.5f, lv) / d;
+	return q4(axis.x * s, axis.y * s, axis.z * s, cos_f(angle * 0.5f, lv));
 }
 // IKKusudama3D::get_quaternion_axis_angle (ik_kusudama_3d.cpp:417-427): divides by |axis|^2
-GDI Q axis_angle_sq(V3 axis, float angle) {
+GDI Q axis_angle_sq(V3 axis, float angle, int lv = LIBM_FMA) {
 	float d = length_sq(axis);
 	if (d == 0) return qid();
-	float sin_angle = sin_f(angle * 0.5f);
-	float cos_angle = cos_f(angle * 0.5f);
+	float sin_angle = sin_f(angle * 0.5f, lv);
+	float cos_angle = cos_f(angle * 0.5f, lv);
 	float s = sin_angle / d;
 	return q4(axis.x * s, axis.y * s, axis.z * s, cos_angle);
 }
@@ -599,14 +616,14 @@ GDI V3 get_scale(const B3 &b) {
 	return v3(length(col(b, 0)), length(col(b, 1)), length(col(b, 2))) * sg;
 }
 // Basis(axis, angle)
-GDI B3 axis_angle_basis(V3 axis, float angle) {
+GDI B3 axis_angle_basis(V3 axis, float angle, int lv = LIBM_FMA) {
 	B3 b;
 	V3 sq = v3(axis.x * axis.x, axis.y * axis.y, axis.z * axis.z);
-	float c = cos_f(angle);
+	float c = cos_f(angle, lv);
 	b.r[0].x = sq.x + c * (1.0f - sq.x);
 	b.r[1].y = sq.y + c * (1.0f - sq.y);
 	b.r[2].z = sq.z + c * (1.0f - sq.z);
-	float s = sin_f(angle);
+	float s = sin_f(angle, lv);
 	float t = 1 - c;
 	float xyzt = axis.x * axis.y * t, zyxs = axis.z * s;
 	b.r[0].y = xyzt - zyxs;

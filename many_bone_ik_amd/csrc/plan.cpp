@@ -491,6 +491,7 @@ SetupView setup_view(const HostPlan &p, int32_t n, int32_t max_cones_in) {
 	v.N = n;
 	v.max_cones_in = max_cones_in;
 	v.desc_constraint_count = p.desc_constraint_count;
+	v.libm = p.libm_variant;
 	v.cfs = p.cf_stride();
 	v.cds = p.cd_stride();
 	v.n_topo = (int)p.setup_topo.size();

@@ -90,6 +90,7 @@ struct HostPlan {
 	std::vector<int32_t> setup_topo;                // bones, parents before children
 	std::vector<int32_t> ik_child_off, ik_children; // IK children of each bone, ascending (setup.h)
 	int32_t setup_max_cones = 1;                    // cones stride of the setup inputs
+	int32_t libm_variant = 0;                       // reference host's glibc sinf/cosf build (gd::LIBM_FMA / LIBM_SSE2)
 	int32_t max_headings = 0;
 	// constraint_mode node caches: pre-order position and subtree size of each list bone in
 	// the pose-node forest (-1 / 0 elsewhere), deepest pose chain, positions used.

@@ -34,6 +34,7 @@ struct SetupView {
 	const int *bone_flags, *bone_pose_parent, *bone_ik_parent;
 	const int *ik_child_off, *ik_children; // IK children of each bone, ascending
 	const int *cons_order, *cons_order_slot, *cons_order_ncones, *cons_bone;
+	int libm = LIBM_FMA; // the reference host's glibc sinf/cosf build (HostPlan::libm_variant)
 };
 
 // Scratch one skeleton's setup needs (callers size it with setup_scratch_bytes).
@@ -130,7 +131,7 @@ GDI void set_control_point(Cone &c, V3 v) {
 	if (is_zero_approx(length_sq(v))) c.cp = v3(0, 1, 0);
 	else c.cp = normalized(v);
 }
-GDI void update_tangent_handles(Cone &c, const Cone *next) {
+GDI void update_tangent_handles(Cone &c, const Cone *next, int lv) {
 	if (!next) return;
 	double radA = c.radius, radB = next->radius;
 	V3 A = c.cp, Bv = next->cp;
@@ -138,11 +139,11 @@ GDI void update_tangent_handles(Cone &c, const Cone *next) {
 	double tRadius = (gd::PI - (radA + radB)) / 2;
 	double bA = radA + tRadius, bB = radB + tRadius;
 	V3 scaledAxisA = A * (float)::cos(bA);
-	V3 planeDir1A = xform(axis_angle_sq(arc_normal, (float)bA), A);
-	V3 planeDir2A = xform(axis_angle_sq(A, (float)(gd::PI / 2)), planeDir1A);
+	V3 planeDir1A = xform(axis_angle_sq(arc_normal, (float)bA, lv), A);
+	V3 planeDir2A = xform(axis_angle_sq(A, (float)(gd::PI / 2), lv), planeDir1A);
 	V3 scaledAxisB = Bv * (float)::cos(bB);
-	V3 planeDir1B = xform(axis_angle_sq(arc_normal, (float)bB), Bv);
-	V3 planeDir2B = xform(axis_angle_sq(Bv, (float)(gd::PI / 2)), planeDir1B);
+	V3 planeDir1B = xform(axis_angle_sq(arc_normal, (float)bB, lv), Bv);
+	V3 planeDir2B = xform(axis_angle_sq(Bv, (float)(gd::PI / 2), lv), planeDir1B);
 	Ray r1B{planeDir1B, scaledAxisB}, r2B{planeDir1B, planeDir2B};
 	elongate(r1B, 99);
 	elongate(r2B, 99);
@@ -159,8 +160,8 @@ GDI void update_tangent_handles(Cone &c, const Cone *next) {
 	if (is_zero_approx(length_sq(c.t1))) c.t1 = normalized(get_orthogonal(c.cp));
 	if (is_zero_approx(length_sq(c.t2))) c.t2 = normalized(get_orthogonal(c.t1 * -1.0f));
 }
-GDI void update_tangent_radii(Cone *cs, int n) {
-	for (int i = 0; i < n; i++) update_tangent_handles(cs[i], i + 1 < n ? &cs[i + 1] : nullptr);
+GDI void update_tangent_radii(Cone *cs, int n, int lv) {
+	for (int i = 0; i < n; i++) update_tangent_handles(cs[i], i + 1 < n ? &cs[i + 1] : nullptr, lv);
 }
 
 // Setup of one skeleton: reads its setup pose [B][10] and entry s_in of cones
@@ -232,16 +233,16 @@ GDI void setup_skeleton(const SetupView &v, int s_in, int s, const float *pose, 
 			cone.rcos = ::cos(cone.radius);
 			set_control_point(cone, normalized(v3(cn[4 * k], cn[4 * k + 1], cn[4 * k + 2])));
 			cs[ncs++] = cone;
-			update_tangent_radii(cs, ncs);
+			update_tangent_radii(cs, ncs, v.libm);
 		}
 		// set_axial_limits (ik_kusudama_3d.cpp:103-115)
 		float min_angle = tw[0], range = tw[1];
 		V3 y_axis = v3(0, 1, 0), z_axis = v3(0, 0, 1);
-		Q twist_min_rot = axis_angle_sq(y_axis, min_angle);
+		Q twist_min_rot = axis_angle_sq(y_axis, min_angle, v.libm);
 		V3 twist_min_vec = normalized(xform(twist_min_rot, z_axis));
 		V3 twist_center_vec = normalized(xform(twist_min_rot, twist_min_vec));
 		w.tcr[slot] = arc(z_axis, twist_center_vec);
-		w.thc[slot] = cos_f(range / 4.0f);
+		w.thc[slot] = cos_f(range / 4.0f, v.libm);
 		// _update_constraint(twist node) (ik_kusudama_3d.cpp:37-89)
 		V3 sum = v3(0, 0, 0);
 		int nd = 0;
@@ -253,7 +254,7 @@ GDI void setup_skeleton(const SetupView &v, int s_in, int s, const float *pose, 
 				Q ttn = arc(cs[k].cp, cs[k + 1].cp);
 				V3 axis = get_axis(ttn);
 				double angle = get_angle(ttn) / 2.0;
-				V3 half = xform(axis_angle_basis(axis, (float)angle), cs[k].cp);
+				V3 half = xform(axis_angle_basis(axis, (float)angle, v.libm), cs[k].cp);
 				half = half * get_angle(ttn);
 				half = normalized(half);
 				sum = sum + half;
@@ -270,7 +271,7 @@ GDI void setup_skeleton(const SetupView &v, int s_in, int s, const float *pose, 
 			w.T[slot] = ((inverse(Pb) * from_quat(otn)) * Pb) * w.T[slot];
 		}
 		for (int k = 0; k < ncs; k++) set_control_point(cs[k], normalized(cs[k].cp));
-		update_tangent_radii(cs, ncs);
+		update_tangent_radii(cs, ncs, v.libm);
 		for (int k = 0; k < ncs; k++) w.kc[(size_t)slot * mc + k] = cs[k];
 		w.kcn[slot] = ncs;
 	}
@@ -288,10 +289,10 @@ GDI void setup_skeleton(const SetupView &v, int s_in, int s, const float *pose, 
 			const int o = CF_CONE0 + CF_PER_CONE * k;
 			const float rf = (float)c.radius, trf = (float)c.tr;
 			cf[(o + 0) * N] = c.cp.x; cf[(o + 1) * N] = c.cp.y; cf[(o + 2) * N] = c.cp.z;
-			cf[(o + 3) * N] = sin_f(rf * 0.5f); cf[(o + 4) * N] = cos_f(rf * 0.5f);
+			cf[(o + 3) * N] = sin_f(rf * 0.5f, v.libm); cf[(o + 4) * N] = cos_f(rf * 0.5f, v.libm);
 			cf[(o + 5) * N] = c.t1.x; cf[(o + 6) * N] = c.t1.y; cf[(o + 7) * N] = c.t1.z;
 			cf[(o + 8) * N] = c.t2.x; cf[(o + 9) * N] = c.t2.y; cf[(o + 10) * N] = c.t2.z;
-			cf[(o + 11) * N] = sin_f(trf * 0.5f); cf[(o + 12) * N] = cos_f(trf * 0.5f);
+			cf[(o + 11) * N] = sin_f(trf * 0.5f, v.libm); cf[(o + 12) * N] = cos_f(trf * 0.5f, v.libm);
 			const V3 ncp = normalized(c.cp);
 			cf[(o + CFC_NCP) * N] = ncp.x; cf[(o + CFC_NCP + 1) * N] = ncp.y; cf[(o + CFC_NCP + 2) * N] = ncp.z;
 			if (k + 1 < w.kcn[slot]) {

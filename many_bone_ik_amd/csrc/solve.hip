@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstddef>
 #include <tuple>
 #include <type_traits>
 #include <cstdio>
@@ -80,6 +81,7 @@ struct DevPlan {
 	int hs_floats;       // staged-heading LDS floats per skeleton
 	int n_gck;           // checkpoint globals per skeleton (HostPlan::bone_gslot)
 	int constraint_mode; // ManyBoneIK3D::constraint_mode
+	int libm;            // the reference host's glibc sinf/cosf build (gd::LIBM_FMA / LIBM_SSE2)
 	int topo_words; // blob size in 32-bit words (multiple of 4)
 	const uint4 *topo_blob;
 #define MBIK_DECL(T, name) const T *name; int o_##name;
@@ -232,6 +234,9 @@ __device__ __forceinline__ BPtr<T> uplus(BPtr<T> p, int k, int area = 0xFF) {
 		return BPtr<T>{p.r, p.o, p.so + (uint32_t)(k * (int)sizeof(T)), p.d};
 #endif
 	}
+#ifdef MBIK_SOFF_STRICT
+	return BPtr<T>{p.r, p.o + p.so + (uint32_t)(k * (int)sizeof(T)), 0u, p.d}; // areas outside the mask: no SGPR part
+#endif
 #endif
 	(void)area;
 	return p + k;
@@ -394,7 +399,7 @@ __device__ __forceinline__ SlerpTo slerp_to(const B3 &to_b) {
 	for (int i = 0; i < 3; i++) r.len[i] = length(to_b.r[i]);
 	return r;
 }
-__device__ __forceinline__ B3 slerp_weight0(const B3 &from_b, const SlerpTo &tt) {
+__device__ __forceinline__ B3 slerp_weight0(const B3 &from_b, const SlerpTo &tt, int lv) {
 	Q from = get_quaternion(from_b);
 	Q to = tt.q;
 	float cosom = dot(from, to);
@@ -406,7 +411,7 @@ __device__ __forceinline__ B3 slerp_weight0(const B3 &from_b, const SlerpTo &tt)
 	float scale0, scale1;
 	if ((1.0f - cosom) > (float)CMP_EPSILON) {
 		// scale1 = sinf(0 * omega) / sinom is +0 for the finite omega of this branch
-		scale0 = slerp_scale0(acos_f(cosom));
+		scale0 = slerp_scale0(acos_f(cosom), lv);
 		scale1 = 0.0f;
 	} else {
 		scale0 = 1.0f;
@@ -1123,7 +1128,7 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 	MBIK_PROF_T(pc0);
 	MBIK_PROF_ADD(11, pt1, pc0);
 #ifndef MBIK_ABLATE_SLERP
-	rot = slerp_weight0(rot, sto);
+	rot = slerp_weight0(rot, sto, t.libm);
 #endif
 	MBIK_PROF_T(pc1);
 	MBIK_PROF_ADD(12, pc0, pc1);
@@ -2011,9 +2016,27 @@ int32_t mbik_describe_topology(const mbik_skeleton_desc *desc, const mbik_config
 	return h.NS;
 }
 
+// mbik_plan_options: NULL = the defaults; fields past struct_size keep theirs.
+static int read_options(const mbik_plan_options *opts, int &libm) {
+	libm = MBIK_LIBM_VARIANT_FMA;
+	if (!opts) return MBIK_OK;
+	if (opts->struct_size < (int32_t)sizeof(int32_t)) return fail(MBIK_EINVAL, "mbik_plan_options.struct_size too small");
+	if (opts->struct_size >= (int32_t)(offsetof(mbik_plan_options, libm_variant) + sizeof(int32_t))) libm = opts->libm_variant;
+	if (libm != MBIK_LIBM_VARIANT_FMA && libm != MBIK_LIBM_VARIANT_SSE2) return fail(MBIK_EINVAL, "unknown libm_variant");
+	return MBIK_OK;
+}
+
 int32_t mbik_plan_create(const mbik_skeleton_desc *desc, const mbik_config *config, int32_t n_skeletons, const float *setup_pose,
 		const float *cones, const float *twist, int32_t device, mbik_plan **out_plan) {
+	return mbik_plan_create_opts(desc, config, nullptr, n_skeletons, setup_pose, cones, twist, device, out_plan);
+}
+
+int32_t mbik_plan_create_opts(const mbik_skeleton_desc *desc, const mbik_config *config, const mbik_plan_options *opts,
+		int32_t n_skeletons, const float *setup_pose, const float *cones, const float *twist, int32_t device,
+		mbik_plan **out_plan) {
 	if (!desc || !config || !out_plan) return fail(MBIK_EINVAL, "null argument");
+	int libm = 0;
+	if (read_options(opts, libm)) return MBIK_EINVAL;
 	*out_plan = nullptr;
 	int ndev = 0;
 	if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(MBIK_ENODEV, "no HIP device visible");
@@ -2025,6 +2048,7 @@ int32_t mbik_plan_create(const mbik_skeleton_desc *desc, const mbik_config *conf
 	keep_inputs(p.get(), *desc, *config);
 	std::string err = mbik::build_topology(*desc, *config, p->host);
 	if (!err.empty()) return fail(MBIK_EINVAL, err);
+	p->host.libm_variant = libm;
 	err = mbik::build_skeletons(p->host, n_skeletons, setup_pose, cones, twist, std::max(1, desc->max_cones));
 	if (!err.empty()) return fail(MBIK_EINVAL, err);
 	const int rc = finish_plan(p.get(), setup_pose, nullptr);
@@ -2068,6 +2092,7 @@ int finish_plan(mbik_plan *p, const float *setup_pose, const void *cm_state) {
 	d.B = h.B; d.P = h.P; d.NS = h.NS; d.NC = h.NC; d.max_cones = h.max_cones; d.N = h.N;
 	d.cf_stride = h.cf_stride(); d.cd_stride = h.cd_stride();
 	d.stab = h.stabilization_passes; d.constraint_mode = h.constraint_mode; d.hs_floats = h.hs_floats;
+	d.libm = h.libm_variant;
 	d.n_gck = h.n_gck;
 	d.lds_stride = (mbik::lds_floats_per_skeleton(h) + 3) & ~3;
 	int rc = 0;
@@ -2306,8 +2331,16 @@ int32_t mbik_selftest_topology(int32_t n_rigs, const mbik_skeleton_desc *descs, 
 int32_t mbik_plan_create_device(int32_t n_rigs, const mbik_skeleton_desc *descs, const mbik_config *configs,
 		const int32_t *n_skeletons, const float *const *setup_pose, const float *const *cones, const float *const *twist,
 		int32_t device, mbik_plan **out_plans) {
+	return mbik_plan_create_device_opts(n_rigs, descs, configs, nullptr, n_skeletons, setup_pose, cones, twist, device, out_plans);
+}
+
+int32_t mbik_plan_create_device_opts(int32_t n_rigs, const mbik_skeleton_desc *descs, const mbik_config *configs,
+		const mbik_plan_options *opts, const int32_t *n_skeletons, const float *const *setup_pose, const float *const *cones,
+		const float *const *twist, int32_t device, mbik_plan **out_plans) {
 	if (n_rigs <= 0 || !descs || !configs || !n_skeletons || !setup_pose || !out_plans) return fail(MBIK_EINVAL, "null argument");
 	for (int i = 0; i < n_rigs; i++) out_plans[i] = nullptr;
+	int libm = 0;
+	if (read_options(opts, libm)) return MBIK_EINVAL;
 	int ndev = 0;
 	if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(MBIK_ENODEV, "no HIP device visible");
 	if (device < 0 || device >= ndev) return fail(MBIK_EINVAL, "device index out of range");
@@ -2336,6 +2369,7 @@ int32_t mbik_plan_create_device(int32_t n_rigs, const mbik_skeleton_desc *descs,
 		keep_inputs(p.get(), d, configs[i]);
 		mbik::HostPlan &h = p->host;
 		h = std::move(built[i]);
+		h.libm_variant = libm;
 		h.N = n_skeletons[i];
 		const size_t N = (size_t)h.N;
 		h.D.assign((size_t)h.B * 9 * N, 0.0f); // filled on the device below (mbik_setup_kernel)
@@ -2360,7 +2394,7 @@ int32_t mbik_plan_create_device(int32_t n_rigs, const mbik_skeleton_desc *descs,
 // ---- plan serialisation (mbik_plan_save / mbik_plan_load) ----
 namespace {
 constexpr char kPlanMagic[8] = {'M', 'B', 'I', 'K', 'P', 'L', 'A', 'N'};
-constexpr uint32_t kPlanFormat = 2; // 2: the table-addressing override joins the layout overrides (1 is still read)
+constexpr uint32_t kPlanFormat = 3; // 2: + the table-addressing override; 3: + libm_variant (1 and 2 are still read)
 struct PlanWriter {
 	std::vector<char> b;
 	void bytes(const void *v, size_t n) {
@@ -2453,6 +2487,7 @@ int32_t mbik_plan_save(const mbik_plan *p, void *buf, uint64_t capacity, uint64_
 			return fail(MBIK_EHIP, "hipMemcpy constraint_mode state");
 	}
 	w.vec(cm);
+	w.put<int32_t>(h.libm_variant); // format 3
 	*size = w.b.size();
 	if (!buf) return MBIK_OK;
 	if (capacity < w.b.size()) return fail(MBIK_EINVAL, "buffer smaller than the saved plan (see *size)");
@@ -2471,7 +2506,7 @@ int32_t mbik_plan_load(const void *buf, uint64_t size, int32_t device, mbik_plan
 	if (!r.bytes(magic, 8) || std::memcmp(magic, kPlanMagic, 8) != 0) return fail(MBIK_EINVAL, "not a saved mbik plan");
 	const uint32_t format = r.get<uint32_t>();
 	if (!r.ok) return fail(MBIK_EINVAL, "truncated or corrupt saved plan");
-	if (format != kPlanFormat && format != 1) return fail(MBIK_EUNSUPPORTED, "saved plan format version not supported");
+	if (format < 1 || format > kPlanFormat) return fail(MBIK_EUNSUPPORTED, "saved plan format version not supported");
 	(void)r.get<uint32_t>(); // the ABI version that wrote it (informational)
 	const int32_t N = r.get<int32_t>();
 	constexpr uint64_t kMax = 1ull << 34;
@@ -2492,7 +2527,9 @@ int32_t mbik_plan_load(const void *buf, uint64_t size, int32_t device, mbik_plan
 	int32_t ov[8] = {};
 	for (int i = 0; i < (format >= 2 ? 8 : 7); i++) ov[i] = r.get<int32_t>();
 	std::vector<char> cm = r.vec<char>(kMax);
+	const int32_t libm = format >= 3 ? r.get<int32_t>() : MBIK_LIBM_VARIANT_FMA;
 	if (!r.ok || N <= 0) return fail(MBIK_EINVAL, "truncated or corrupt saved plan");
+	if (libm != MBIK_LIBM_VARIANT_FMA && libm != MBIK_LIBM_VARIANT_SSE2) return fail(MBIK_EINVAL, "saved plan: unknown libm_variant");
 	mbik_skeleton_desc desc{};
 	desc.bone_count = (int32_t)p->src_parents.size();
 	desc.parents = p->src_parents.data();
@@ -2508,6 +2545,7 @@ int32_t mbik_plan_load(const void *buf, uint64_t size, int32_t device, mbik_plan
 	mbik::HostPlan &h = p->host;
 	std::string err = mbik::build_topology(desc, cfg, h);
 	if (!err.empty()) return fail(MBIK_EINVAL, "saved plan: " + err);
+	h.libm_variant = libm;
 	h.N = N;
 	const size_t n = (size_t)N;
 	if (D.size() != (size_t)h.B * 9 * n || CF.size() != (size_t)h.NC * h.cf_stride() * n ||
@@ -2576,6 +2614,7 @@ int32_t mbik_plan_get_info(const mbik_plan *p, mbik_plan_info *o) {
 	o->constraint_slots = h.NC;
 	o->cf_stride = h.cf_stride();
 	o->cd_stride = h.cd_stride();
+	o->libm_variant = h.libm_variant;
 	return MBIK_OK;
 }
 
@@ -3039,10 +3078,12 @@ __global__ void mbik_selftest_libm_kernel(int fn, uint64_t first, uint64_t count
 	for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += nthreads) {
 		const float x = __uint_as_float((unsigned)(first + i));
 		bool ok, exact;
-		if (fn <= MBIK_LIBM_SLERP_SCALE0) {
+		const bool f32 = fn <= MBIK_LIBM_SLERP_SCALE0 || fn >= MBIK_LIBM_SINF_SSE2;
+		if (f32) {
 			const float e = static_cast<const float *>(expected)[i];
 			const float g = fn == MBIK_LIBM_SINF ? sin_f(x) : fn == MBIK_LIBM_COSF ? cos_f(x) : fn == MBIK_LIBM_ACOSF ? acos_f(x)
-																							: slerp_scale0(x);
+					: fn == MBIK_LIBM_SLERP_SCALE0 ? slerp_scale0(x) : fn == MBIK_LIBM_SINF_SSE2 ? sin_f(x, LIBM_SSE2)
+					: fn == MBIK_LIBM_COSF_SSE2 ? cos_f(x, LIBM_SSE2) : slerp_scale0(x, LIBM_SSE2);
 			ok = exact = same_bits(e, g);
 		} else {
 			const double e = static_cast<const double *>(expected)[i];
@@ -3119,7 +3160,7 @@ int32_t mbik_selftest_div(int32_t device, uint64_t random_iterations, uint64_t o
 int32_t mbik_selftest_libm(int32_t fn, uint64_t first, uint64_t count, const double *inputs, const void *expected,
 		uint64_t out[3], void *hip_stream) {
 	if (!out || !expected) return fail(MBIK_EINVAL, "null argument");
-	if (fn < MBIK_LIBM_SINF || fn > MBIK_LIBM_COS_F64) return fail(MBIK_EINVAL, "unknown function code");
+	if (fn < MBIK_LIBM_SINF || fn > MBIK_LIBM_SLERP_SCALE0_SSE2) return fail(MBIK_EINVAL, "unknown function code");
 	if (fn == MBIK_LIBM_COS_F64 ? !inputs : first + count > (1ull << 32)) return fail(MBIK_EINVAL, "input range");
 	out[0] = 0;
 	out[1] = ~0ull;

@@ -12,7 +12,7 @@ import math
 import numpy as np
 
 from . import _lib
-from ._lib import MbikConfig, MbikConstraint, MbikPin, MbikPlanInfo, MbikSkeletonDesc, check
+from ._lib import MbikConfig, MbikConstraint, MbikPin, MbikPlanInfo, MbikPlanOptions, MbikSkeletonDesc, check
 
 
 def _ptr(a):
@@ -101,7 +101,8 @@ def topology_selftest(rigs, device: int = -1):
     return [int(out[i]) for i in range(len(rigs))], _lib.last_error()
 
 
-def plans_from_device(rigs, n_skeletons, setup_pose_ptrs, cones_ptrs=None, twist_ptrs=None, device: int = 0):
+def plans_from_device(rigs, n_skeletons, setup_pose_ptrs, cones_ptrs=None, twist_ptrs=None, device: int = 0,
+                      libm_variant: int = 0):
     """mbik_plan_create_device: one Plan per rig, topology and setup built on the GPU from
     device buffers (setup poses, cones, twist: device pointers, 0 / None where a rig has no
     constraints)."""
@@ -111,8 +112,9 @@ def plans_from_device(rigs, n_skeletons, setup_pose_ptrs, cones_ptrs=None, twist
     vpa = C.c_void_p * n
     out = vpa()
     ptrs = lambda xs: vpa(*[(x or None) for x in (xs or [0] * n)])
-    check(L.mbik_plan_create_device(n, descs, cfgs, (C.c_int32 * n)(*n_skeletons), ptrs(setup_pose_ptrs), ptrs(cones_ptrs),
-                                    ptrs(twist_ptrs), int(device), out))
+    opts = MbikPlanOptions(C.sizeof(MbikPlanOptions), int(libm_variant))
+    check(L.mbik_plan_create_device_opts(n, descs, cfgs, C.byref(opts), (C.c_int32 * n)(*n_skeletons), ptrs(setup_pose_ptrs),
+                                         ptrs(cones_ptrs), ptrs(twist_ptrs), int(device), out))
     plans = []
     for i, (parents, pins, constraints, kw) in enumerate(rigs):
         p = Plan.__new__(Plan)
@@ -131,7 +133,7 @@ class Plan:
 
     def __init__(self, parents, pins, constraints, setup_pose, cones=None, twist=None, *,
                  iterations=15, default_damp=math.radians(5.0), constraint_mode=False,
-                 stabilization_passes=0, bone_damp=None, max_cones=None, device=0, lanes=0):
+                 stabilization_passes=0, bone_damp=None, max_cones=None, device=0, lanes=0, libm_variant=0):
         L = _lib.load()
         self._L = L
         setup_pose = np.ascontiguousarray(setup_pose, np.float32)
@@ -143,8 +145,9 @@ class Plan:
         cones_a = None if cones is None else np.ascontiguousarray(cones, np.float32)
         twist_a = None if twist is None else np.ascontiguousarray(twist, np.float32)
         h = C.c_void_p()
-        check(L.mbik_plan_create(C.byref(d.desc), C.byref(d.cfg), n, _ptr(setup_pose), _ptr(cones_a), _ptr(twist_a),
-                                 int(device), C.byref(h)))
+        opts = MbikPlanOptions(C.sizeof(MbikPlanOptions), int(libm_variant))
+        check(L.mbik_plan_create_opts(C.byref(d.desc), C.byref(d.cfg), C.byref(opts), n, _ptr(setup_pose), _ptr(cones_a),
+                                      _ptr(twist_a), int(device), C.byref(h)))
         self.h = h
         self.n = n
         self.B = B
@@ -160,13 +163,14 @@ class Plan:
             self.set_launch(lanes)
 
     @classmethod
-    def from_workload(cls, wl, device=0, lanes=0, iterations=None, stabilization_passes=0, constraint_mode=False):
+    def from_workload(cls, wl, device=0, lanes=0, iterations=None, stabilization_passes=0, constraint_mode=False,
+                      libm_variant=0):
         t = wl.topo
         return cls(t.parents, wl.pins(), wl.constraints(), wl.pose, wl.cones, wl.twist,
                    iterations=t.iterations if iterations is None else iterations,
                    default_damp=wl.default_damp, max_cones=wl.cones.shape[2], device=device, lanes=lanes,
                    bone_damp=wl.bone_damp, stabilization_passes=stabilization_passes,
-                   constraint_mode=constraint_mode)
+                   constraint_mode=constraint_mode, libm_variant=libm_variant)
 
     def save(self) -> bytes:
         """mbik_plan_save: the plan as a flat binary (topology inputs, setup tables, layout,

@@ -39,3 +39,45 @@ def test_libm_fill_matches_restatement(oracle):
     assert v.dtype == np.float32 and np.isfinite(v).all()
     n, _ = oracle.libm_restated_mismatches(0, int(np.float32(0.25).view(np.uint32)), 1 << 16, 1)
     assert n == 0
+
+
+def _gdmath_checker():
+    """tools/gdmath_host_check.cpp: the product's own gd_math.h (host build) vs the platform libm."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "build", "gdmath_host_check_test")
+    src = os.path.join(root, "tools", "gdmath_host_check.cpp")
+    os.makedirs(os.path.dirname(exe), exist_ok=True)
+    if not os.path.exists(exe) or os.path.getmtime(exe) < max(os.path.getmtime(src), os.path.getmtime(
+            os.path.join(root, "many_bone_ik_amd", "csrc", "gd_math.h"))):
+        subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-fno-builtin", "-pthread", "-I",
+                        os.path.join(root, "many_bone_ik_amd", "csrc"), src, "-o", exe], check=True)
+    return exe
+
+
+def _run_checker(variant, sse2_platform, *args):
+    import os
+    import re
+    import subprocess
+    from many_bone_ik_amd import _lib
+    env = dict(os.environ)
+    env.pop("GLIBC_TUNABLES", None)
+    if sse2_platform:
+        env["GLIBC_TUNABLES"] = _lib.GLIBC_SSE2_TUNABLES
+    out = subprocess.run([_gdmath_checker(), str(variant), *args], capture_output=True, text=True, env=env,
+                         check=True).stdout
+    return {m.group(1): int(m.group(2)) for m in re.finditer(r"^(\w+)\s+variant \w+ mismatches .*?: (\d+)", out, re.M)}
+
+
+@pytest.mark.parametrize("variant,sse2_platform", [(0, False), (1, True)])
+def test_product_libm_variants_match_their_glibc_build(variant, sse2_platform):
+    """gd_math.h's sinf/cosf (the kernel's source, host build) in each libm_variant equal the
+    platform glibc built the same way -- the FMA build by default, the SSE2 build when
+    GLIBC_TUNABLES disables the FMA ifunc -- on a strided sweep and on the discriminating
+    inputs; the other pairing differs on those inputs (so the tunable really switches)."""
+    disc = FMA_DISCRIMINATING[0] + FMA_DISCRIMINATING[1]
+    assert all(v == 0 for v in _run_checker(variant, sse2_platform, "4099").values())
+    assert all(v == 0 for v in _run_checker(variant, sse2_platform, "list", *disc).values())
+    crossed = _run_checker(1 - variant, sse2_platform, "list", *disc)
+    assert crossed["sin_f"] == 4 and crossed["cos_f"] == 4 and crossed["acos_f"] == 0
