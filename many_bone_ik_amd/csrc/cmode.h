@@ -37,6 +37,11 @@ struct CmodeState {
 
 enum { CK_POSE = 0, CK_BDIR = 1, CK_COR = 2, CK_CTW = 3 };
 
+// NB32: the node area is below 4 GiB (the usual case; cmode_node_fits_32), so a node read is a
+// buffer load per element -- the slot's lane offset k * 48 N + 4 s in one VGPR, the element's
+// f * 4 N in the instruction's SGPR offset -- with no per-element address arithmetic; else
+// 64-bit addresses.
+template <bool NB32>
 struct CmodeLane {
 	const DevPlan &t;
 	const CmodeState &c;
@@ -49,29 +54,39 @@ struct CmodeLane {
 	const int *pre, *sub; // LDS copies
 	int lo, hi;           // pre-order range this lane may write (its segment root's subtree)
 	int *pend;            // pose node whose dirty chain this lane read privately (-1 none)
+	__amdgpu_buffer_rsrc_t r; // NB32: the whole node area
+	uint32_t s4;          // NB32: 4 s
 
 	__device__ __forceinline__ float *slot(int k) const { return node + (size_t)k * 12 * fs; }
 	__device__ __forceinline__ X3 ld(int k) const {
-		const float *p = slot(k);
-		const size_t N = fs;
 		X3 x;
+		float v[12];
+		if constexpr (NB32) {
+			const uint32_t N4 = (uint32_t)fs * 4u, o = (uint32_t)k * 12u * N4 + s4;
 #pragma unroll
-		for (int i = 0; i < 3; i++) x.b.r[i] = v3(p[(3 * i) * N], p[(3 * i + 1) * N], p[(3 * i + 2) * N]);
-		x.o = v3(p[9 * N], p[10 * N], p[11 * N]);
+			for (int f = 0; f < 12; f++) v[f] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, o, (uint32_t)f * N4, 0));
+		} else {
+			const float *p = slot(k);
+#pragma unroll
+			for (int f = 0; f < 12; f++) v[f] = p[(size_t)f * fs];
+		}
+#pragma unroll
+		for (int i = 0; i < 3; i++) x.b.r[i] = v3(v[3 * i], v[3 * i + 1], v[3 * i + 2]);
+		x.o = v3(v[9], v[10], v[11]);
 		return x;
 	}
 	__device__ __forceinline__ void st(int k, const X3 &x) const {
-		float *p = slot(k);
-		const size_t N = fs;
+		const float v[12] = {x.b.r[0].x, x.b.r[0].y, x.b.r[0].z, x.b.r[1].x, x.b.r[1].y, x.b.r[1].z,
+				x.b.r[2].x, x.b.r[2].y, x.b.r[2].z, x.o.x, x.o.y, x.o.z};
+		if constexpr (NB32) {
+			const uint32_t N4 = (uint32_t)fs * 4u, o = (uint32_t)k * 12u * N4 + s4;
 #pragma unroll
-		for (int i = 0; i < 3; i++) {
-			p[(3 * i) * N] = x.b.r[i].x;
-			p[(3 * i + 1) * N] = x.b.r[i].y;
-			p[(3 * i + 2) * N] = x.b.r[i].z;
+			for (int f = 0; f < 12; f++) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v[f]), r, o, (uint32_t)f * N4, 0);
+		} else {
+			float *p = slot(k);
+#pragma unroll
+			for (int f = 0; f < 12; f++) p[(size_t)f * fs] = v[f];
 		}
-		p[9 * N] = x.o.x;
-		p[10 * N] = x.o.y;
-		p[11 * N] = x.o.z;
 	}
 	__device__ __forceinline__ int LP(int b) const { return b; }
 	__device__ __forceinline__ int GP(int b) const { return t.B + b; }
@@ -123,12 +138,20 @@ struct CmodeLane {
 			if (pp < 0 || !dirty(CK_POSE, pp)) break;
 			x = pp;
 		}
+		// Top-down over stk[n-1] (= x) .. stk[0] (= b).  The chain's locals are known now, so
+		// their loads run two nodes ahead of the products: a chain of n dependent node-cache
+		// misses becomes ~n/3 round trips (the products and their order are unchanged).
 		const X3 Lx = ld(LP(x));
+		X3 La = n >= 2 ? ld(LP(stk[64 * (n - 2)])) : Lx;
+		X3 Lb = n >= 3 ? ld(LP(stk[64 * (n - 3)])) : Lx;
 		X3 G = pp >= 0 ? ld(GP(pp)) * Lx : (pp == mbik::POSE_PARENT_ORIGIN ? xid() * Lx : Lx);
 		keep(x, G);
 		for (int i = n - 2; i >= 0; i--) {
+			const X3 Lc = La;
+			La = Lb;
+			if (i >= 2) Lb = ld(LP(stk[64 * (i - 2)]));
 			x = stk[64 * i];
-			G = G * ld(LP(x));
+			G = G * Lc;
 			keep(x, G);
 		}
 		return G;
@@ -177,8 +200,8 @@ struct CmodeLane {
 // headings' origins for stabilization), the swing snap (ik_kusudama_3d.cpp:347-376), the
 // twist snap (:117-132) and, for stabilized root segments, the MSD accept / restore loop
 // (ik_bone_segment_3d.cpp:163-180).  OE: the lane's target-heading origins, OE[64 * (3e + i)].
-template <bool STAB>
-__device__ void cmode_step(const CmodeLane &C, int seg, int k, const float *tg, float *OE, double &prev_dev) {
+template <bool STAB, bool NB32>
+__device__ void cmode_step(const CmodeLane<NB32> &C, int seg, int k, const float *tg, float *OE, double &prev_dev) {
 	const int ls = 64;
 	const DevPlan &t = C.t;
 	const int b = t.seg_bones[k];
@@ -287,7 +310,7 @@ __device__ void cmode_step(const CmodeLane &C, int seg, int k, const float *tg, 
 // staging it through LDS was measured slower (one lane per skeleton: C2 5.6 vs 5.1 ms, C5
 // 1003 vs 56 ms; LDS caps how many skeletons are resident;
 // profiles/r01_cmode_layout_sweep.jsonl).
-template <bool STAB>
+template <bool STAB, bool NB32>
 __global__ __launch_bounds__(64) void mbik_cmode_kernel(DevPlan t, CmodeState c, int first, int count,
 		const float *__restrict__ pose_in, const float *__restrict__ targets, float *__restrict__ pose_out, int iterations,
 		int seg_lo, int seg_hi) {
@@ -313,11 +336,13 @@ __global__ __launch_bounds__(64) void mbik_cmode_kernel(DevPlan t, CmodeState c,
 	int *stk0 = reinterpret_cast<int *>(dl0 + (size_t)4 * c.W * spw);
 	float *OE = reinterpret_cast<float *>(stk0 + (size_t)c.maxd * 64) + lane;
 	const int g = lane >> t.log2K, role = lane & (K - 1);
-	const int local = blockIdx.x * spw + g;
+	const int local = xcd_block() * spw + g; // XCD-aware: neighbouring skeletons' node rows share L2 lines
 	const bool valid = local < count;
 	const size_t s = (size_t)first + (valid ? local : 0);
 	int pend = -1;
-	CmodeLane C{t, c, s, c.node + s, (size_t)t.N, dl0 + g, spw, stk0 + lane, pre, sub, 0, 0x7fffffff, &pend};
+	const uint32_t node_bytes = NB32 ? (uint32_t)((size_t)(3 * B + 2 * t.NC) * 12 * t.N * 4) : 0u;
+	CmodeLane<NB32> C{t, c, s, c.node + s, (size_t)t.N, dl0 + g, spw, stk0 + lane, pre, sub, 0, 0x7fffffff, &pend,
+			buf_rsrc(c.node, node_bytes), (uint32_t)s * 4u};
 	if (valid)
 		for (int w = role; w < 4 * c.W; w += K) C.dl[spw * w] = c.dirty[(size_t)w * t.N + s];
 	__syncthreads();
@@ -342,7 +367,7 @@ __global__ __launch_bounds__(64) void mbik_cmode_kernel(DevPlan t, CmodeState c,
 				C.hi = pre[root] + sub[root];
 				double prev_dev = INFINITY; // reset after the segment root bone (:178-180)
 				for (int k = t.seg_bone_off[task.x]; k < t.seg_bone_off[task.x + 1]; k++)
-					cmode_step<STAB>(C, task.x, k, tg, OE, prev_dev);
+					cmode_step<STAB, NB32>(C, task.x, k, tg, OE, prev_dev);
 			}
 			__syncthreads();
 			// The cleaning the reference's first read above the segment root did: the dirty

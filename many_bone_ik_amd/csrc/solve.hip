@@ -1954,10 +1954,15 @@ int launch(mbik_plan *p, int first, int count, const float *pose_in, const float
 		if (clds > 160 * 1024) return fail(MBIK_EUNSUPPORTED, "skeleton too large for the constraint_mode LDS layout");
 		static std::once_flag conce;
 		std::call_once(conce, [] {
-			(void)hipFuncSetAttribute((const void *)mbik_cmode_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-			(void)hipFuncSetAttribute((const void *)mbik_cmode_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+			(void)hipFuncSetAttribute((const void *)mbik_cmode_kernel<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+			(void)hipFuncSetAttribute((const void *)mbik_cmode_kernel<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+			(void)hipFuncSetAttribute((const void *)mbik_cmode_kernel<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+			(void)hipFuncSetAttribute((const void *)mbik_cmode_kernel<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 		});
-		auto ck = h.stabilization_passes > 0 ? mbik_cmode_kernel<true> : mbik_cmode_kernel<false>;
+		// node caches below 4 GiB: buffer-resource addressing (cmode.h, NB32)
+		const bool nb32 = (size_t)(3 * h.B + 2 * h.NC) * 12 * (size_t)h.N * sizeof(float) < (size_t(1) << 32) && !p->tab64;
+		auto ck = h.stabilization_passes > 0 ? (nb32 ? mbik_cmode_kernel<true, true> : mbik_cmode_kernel<true, false>)
+											 : (nb32 ? mbik_cmode_kernel<false, true> : mbik_cmode_kernel<false, false>);
 		const int cspw = 64 >> h.log2K;
 		hipLaunchKernelGGL(ck, dim3((unsigned)((count + cspw - 1) / cspw)), dim3(64), clds, stream, p->dev, p->cm, first, count,
 				pose_in, targets, pose_out, iterations, seg_lo, seg_hi);

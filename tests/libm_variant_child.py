@@ -77,13 +77,15 @@ def parity():
     cases += [("C2_twist_sin", discriminating(base, "sin")), ("C2_twist_cos", discriminating(base, "cos"))]
     for name, wl in cases:
         ref = po.Oracle(wl).solve(wl.pose, wl.targets, threads=8)  # platform libm: the SSE2 build here
-        r = {}
+        r, tables = {}, []
         for v in (0, 1):
             p = Plan.from_workload(wl, libm_variant=v)
             got = p.solve_host(wl.pose, wl.targets)
             assert p.info()["libm_variant"] == v
+            tables.append(p.setup_tables())
             p.close()
             r[f"variant{v}_bitwise"] = bool(np.array_equal(got.view(np.uint32), ref.view(np.uint32)))
+        r["tables_differ"] = any(not np.array_equal(a.view(np.uint8), b.view(np.uint8)) for a, b in zip(*tables))
         out[name] = r
     return out
 

@@ -1,0 +1,111 @@
+// FETCH_SIZE calibration for the access widths the solve kernel uses: the
+// guide validates FETCH_SIZE = 1/2 of the bytes only for 16-B-per-lane streaming reads
+// (MI355X_MICROARCH.md, HBM section).  Each kernel below reads a 1 GiB buffer (4x the
+// 256 MiB Infinity Cache, so nothing is re-served on-die) exactly once, through raw buffer
+// loads like solve.hip's, in one pattern; rocprofv3 --pmc FETCH_SIZE per dispatch against the
+// known byte count gives the correction for that pattern.
+//   hipcc --offload-arch=gfx950 -O3 tools/fetch_calib.hip -o build/fetch_calib
+//   rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/fc -o fc -- build/fetch_calib
+// Kernels (bytes of distinct 128-B lines touched = the buffer, 1 GiB, in every case):
+//   b128_coal  16 B per lane, consecutive (the guide's validated case)
+//   b64_coal   8 B per lane, consecutive
+//   b32_coal   4 B per lane, consecutive
+//   b32_s64    4 B per lane at a 64-B stride, then the other half-lines in a second sweep
+//   b32_s128   4 B per lane, one lane per 128-B line; 32 sweeps cover every dword
+//   b32_tile16 the solve's tiled-table pattern: 16 lanes read 16 consecutive dwords (64 B),
+//              the wave's 4 lane groups 4 different 64-B runs 1 KiB apart
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+
+typedef unsigned int U2 __attribute__((ext_vector_type(2)));
+typedef unsigned int U4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *p, uint32_t bytes) {
+	return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, (int)bytes, 0x00020000);
+}
+
+// Each wave folds what it read into one dword (nothing is optimised away) and stores it.
+__global__ void b128_coal(const uint32_t *p, uint32_t bytes, uint32_t *out) {
+	const auto r = rsrc(p, bytes);
+	uint32_t acc = 0;
+	const uint32_t nthreads = gridDim.x * blockDim.x;
+	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < bytes / 16; i += nthreads) {
+		U4 v = __builtin_amdgcn_raw_buffer_load_b128(r, i * 16, 0, 0);
+		acc ^= v.x ^ v.y ^ v.z ^ v.w;
+	}
+	out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+}
+__global__ void b64_coal(const uint32_t *p, uint32_t bytes, uint32_t *out) {
+	const auto r = rsrc(p, bytes);
+	uint32_t acc = 0;
+	const uint32_t nthreads = gridDim.x * blockDim.x;
+	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < bytes / 8; i += nthreads) {
+		U2 v = __builtin_amdgcn_raw_buffer_load_b64(r, i * 8, 0, 0);
+		acc ^= v.x ^ v.y;
+	}
+	out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+}
+__global__ void b32_coal(const uint32_t *p, uint32_t bytes, uint32_t *out) {
+	const auto r = rsrc(p, bytes);
+	uint32_t acc = 0;
+	const uint32_t nthreads = gridDim.x * blockDim.x;
+	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < bytes / 4; i += nthreads)
+		acc ^= __builtin_amdgcn_raw_buffer_load_b32(r, i * 4, 0, 0);
+	out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+}
+// stride S bytes: sweep k (0 .. S/4-1) reads dword k of every S-byte run
+template <int S>
+__global__ void b32_strided(const uint32_t *p, uint32_t bytes, uint32_t *out) {
+	const auto r = rsrc(p, bytes);
+	uint32_t acc = 0;
+	const uint32_t nthreads = gridDim.x * blockDim.x;
+	for (uint32_t k = 0; k < S / 4; k++)
+		for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < bytes / S; i += nthreads)
+			acc ^= __builtin_amdgcn_raw_buffer_load_b32(r, i * S + 4 * k, 0, 0);
+	out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+}
+// 16 lanes x 4 B = one 64-B run; lane group g of the wave reads run (w * 4 + g) * 16 + ...:
+// the runs of one instruction sit 1 KiB apart (a tiled table: field f of 16 skeletons, next
+// slot's field 1 KiB further), and successive instructions walk the 16 runs between them
+__global__ void b32_tile16(const uint32_t *p, uint32_t bytes, uint32_t *out) {
+	const auto r = rsrc(p, bytes);
+	uint32_t acc = 0;
+	const uint32_t lane = threadIdx.x & 63, g = lane >> 4, l = lane & 15;
+	const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nwaves = (gridDim.x * blockDim.x) >> 6;
+	// a 4 KiB block = 4 groups x 16 runs x 64 B; each wave owns whole blocks
+	for (uint32_t b = wave; b < bytes / 4096; b += nwaves)
+		for (uint32_t k = 0; k < 16; k++) acc ^= __builtin_amdgcn_raw_buffer_load_b32(r, b * 4096 + g * 1024 + k * 64 + l * 4, 0, 0);
+	out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+}
+
+int main() {
+	const uint32_t bytes = 1u << 30;
+	uint32_t *p, *out;
+	const int blocks = 4096, threads = 256;
+	if (hipMalloc(&p, bytes) || hipMalloc(&out, (size_t)blocks * threads * 4)) return 1;
+	if (hipMemset(p, 1, bytes)) return 1;
+	hipEvent_t e0, e1;
+	hipEventCreate(&e0);
+	hipEventCreate(&e1);
+	struct K {
+		const char *name;
+		void (*f)(const uint32_t *, uint32_t, uint32_t *);
+	} ks[] = {{"b128_coal", b128_coal}, {"b64_coal", b64_coal}, {"b32_coal", b32_coal}, {"b32_s64", b32_strided<64>},
+			{"b32_s128", b32_strided<128>}, {"b32_tile16", b32_tile16}};
+	for (const K &k : ks) {
+		for (int rep = 0; rep < 2; rep++) {
+			// (1 GiB is 4x the Infinity Cache: a repeat reads from HBM again)
+			if (hipMemset(out, 0, (size_t)blocks * threads * 4)) return 1;
+			hipEventRecord(e0, 0);
+			hipLaunchKernelGGL(k.f, dim3(blocks), dim3(threads), 0, 0, p, bytes, out);
+			hipEventRecord(e1, 0);
+			if (hipEventSynchronize(e1)) return 1;
+			float ms = 0;
+			hipEventElapsedTime(&ms, e0, e1);
+			printf("%-10s rep %d: %8.3f ms  %7.1f GB/s (1 GiB read once)\n", k.name, rep, ms, bytes / (ms * 1e-3) / 1e9);
+		}
+	}
+	return 0;
+}
