@@ -33,6 +33,8 @@ struct CmodeState {
 	const int *sub;     // [B] subtree size
 	int W;              // dirty words per kind
 	int maxd;           // deepest pose chain
+	int spw = 0;        // skeletons per wave (<= 64 / K; fewer leave lanes idle but put more waves per SIMD)
+	int wpb = 1;        // waves per block: they share the block's LDS copy of the topology
 };
 
 enum { CK_POSE = 0, CK_BDIR = 1, CK_COR = 2, CK_CTW = 3 };
@@ -56,6 +58,9 @@ struct CmodeLane {
 	int *pend;            // pose node whose dirty chain this lane read privately (-1 none)
 	__amdgpu_buffer_rsrc_t r; // NB32: the whole node area
 	uint32_t s4;          // NB32: 4 s
+#ifdef MBIK_PROF
+	uint64_t *pf;         // diagnostic counters (tools/prof_cmode.py): see mbik_cmode_kernel
+#endif
 
 	__device__ __forceinline__ float *slot(int k) const { return node + (size_t)k * 12 * fs; }
 	__device__ __forceinline__ X3 ld(int k) const {
@@ -131,6 +136,7 @@ struct CmodeLane {
 	// recorded in *pend for the after-row cleaning.
 	__device__ X3 pose_global(int b) const {
 		if (!dirty(CK_POSE, b)) return ld(GP(b));
+		MBIK_PROF_T(q0);
 		int n = 0, x = b, pp;
 		for (;;) {
 			stk[64 * n++] = x;
@@ -154,6 +160,12 @@ struct CmodeLane {
 			G = G * Lc;
 			keep(x, G);
 		}
+#ifdef MBIK_PROF
+		MBIK_PROF_T(q1);
+		pf[4] += q1 - q0;
+		pf[5] += n;
+		pf[6] += 1;
+#endif
 		return G;
 	}
 	__device__ __forceinline__ void keep(int x, const X3 &G) const {
@@ -167,6 +179,9 @@ struct CmodeLane {
 	// IKBone3D::get_bone_direction_global_pose (ik_bone_3d.cpp:157-159): local = (D, 0).
 	__device__ X3 bdir_global(int b) const {
 		if (!dirty(CK_BDIR, b)) return ld(GD(b));
+#ifdef MBIK_PROF
+		pf[9] += 1;
+#endif
 		const X3 G = pose_global(b) * X3{ld_soa_basis(t, t.D, b, 9, 0, s), v3(0, 0, 0)};
 		st(GD(b), G);
 		set_clean(CK_BDIR, b);
@@ -208,6 +223,10 @@ __device__ void cmode_step(const CmodeLane<NB32> &C, int seg, int k, const float
 	const int e0 = t.seg_eff_off[seg], e1 = t.seg_eff_off[seg + 1];
 	const bool stab = STAB && (t.seg_flags[seg] & mbik::SF_STAB) != 0;
 	const int flags = t.bone_flags[b];
+#ifdef MBIK_PROF
+	uint64_t *pf = C.pf;
+#endif
+	MBIK_PROF_T(c0);
 	for (int i = e0; i < e1; i++) {
 		const int e = t.seg_effs[i];
 		const X3 E = C.bdir_global(t.eff_bone[e]);
@@ -224,6 +243,8 @@ __device__ void cmode_step(const CmodeLane<NB32> &C, int seg, int k, const float
 			for (int i = e0; i < e1; i++) (void)C.bdir_global(t.eff_bone[t.seg_effs[i]]);
 			(void)C.bdir_global(b);
 		}
+		MBIK_PROF_T(c1);
+		MBIK_PROF_ADD(0, c0, c1);
 		if (flags & mbik::BF_ORIENT) {
 			const int slot_ = t.bone_cons[b];
 			const X3 Gc = C.orient_global(b);
@@ -244,6 +265,8 @@ __device__ void cmode_step(const CmodeLane<NB32> &C, int seg, int k, const float
 				C.set_dirty(CK_POSE, b);
 			}
 		}
+		MBIK_PROF_T(c2);
+		MBIK_PROF_ADD(1, c1, c2);
 		if (flags & mbik::BF_AXIAL) {
 			const int slot_ = t.bone_cons[b];
 			const int cs = t.cf_stride;
@@ -266,6 +289,8 @@ __device__ void cmode_step(const CmodeLane<NB32> &C, int seg, int k, const float
 				C.propagate(b);
 			}
 		}
+		MBIK_PROF_T(c3);
+		MBIK_PROF_ADD(2, c2, c3);
 		if (!stab) break;
 		// _get_manual_msd(tip_headings_uniform, target_headings, weights) (:114-127)
 		const double *hw = t.seg_hw + t.seg_hw_off[seg];
@@ -303,46 +328,61 @@ __device__ void cmode_step(const CmodeLane<NB32> &C, int seg, int k, const float
 }
 
 // _process_modification (many_bone_ik_3d.cpp:645-694) in constraint_mode: K = 2^log2K lanes
-// per skeleton, 64 / K skeletons per one-wave block, the default kernel's sibling-row
-// schedule (t.sched).  LDS: the topology blob, the pre-order tables, the dirty words (4 W per
-// skeleton, interleaved by skeleton), then per lane (interleaved by 64) the chain stack
-// (maxd) and, with STAB, the target-heading origins (3 P).  The node state stays in HBM:
+// per skeleton, c.spw (<= 64 / K) skeletons per wave, c.wpb waves per block, the default
+// kernel's sibling-row schedule (t.sched).  LDS: the topology blob and the pre-order tables
+// once per block, then per wave the dirty words (4 W per skeleton, interleaved by skeleton),
+// per lane (interleaved by 64) the chain stack (maxd) and, with STAB, the target-heading
+// origins (3 P).  The solve is a chain of node-cache reads that miss to HBM (C5: 786 MB of
+// node state), so what pays is memory-level parallelism: several waves per SIMD, which the
+// shared topology copy makes fit in LDS (cmode_autotune times spw x K).  The node state stays in HBM:
 // staging it through LDS was measured slower (one lane per skeleton: C2 5.6 vs 5.1 ms, C5
 // 1003 vs 56 ms; LDS caps how many skeletons are resident;
 // profiles/r01_cmode_layout_sweep.jsonl).
+constexpr int kCmodeMaxWaves = 4; // waves per constraint_mode block (launch bound)
 template <bool STAB, bool NB32>
-__global__ __launch_bounds__(64) void mbik_cmode_kernel(DevPlan t, CmodeState c, int first, int count,
+__global__ __launch_bounds__(64 * kCmodeMaxWaves) void mbik_cmode_kernel(DevPlan t, CmodeState c, int first, int count,
 		const float *__restrict__ pose_in, const float *__restrict__ targets, float *__restrict__ pose_out, int iterations,
 		int seg_lo, int seg_hi) {
 	extern __shared__ float4 lds4[];
-	const int lane = threadIdx.x;
+	const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 	{
 		uint4 *dst = reinterpret_cast<uint4 *>(lds4);
-		for (int i = lane; i < (t.topo_words >> 2); i += 64) dst[i] = t.topo_blob[i];
+		for (int i = threadIdx.x; i < (t.topo_words >> 2); i += blockDim.x) dst[i] = t.topo_blob[i];
 	}
 	const uint32_t *topo = reinterpret_cast<const uint32_t *>(lds4);
 #define MBIK_REPOINT(T, name) t.name = reinterpret_cast<const T *>(topo + t.o_##name);
 	MBIK_TOPO_TABLES(MBIK_REPOINT)
 #undef MBIK_REPOINT
 	const int B = t.B, P = t.P, K = t.K;
-	const int spw = 64 >> t.log2K;
+	const int spw = c.spw; // skeletons of this wave (<= 64 / K)
 	int *pre = reinterpret_cast<int *>(lds4) + t.topo_words;
 	int *sub = pre + B;
-	for (int i = lane; i < B; i += 64) {
+	for (int i = threadIdx.x; i < B; i += blockDim.x) {
 		pre[i] = c.pre[i];
 		sub[i] = c.sub[i];
 	}
-	uint32_t *dl0 = reinterpret_cast<uint32_t *>(sub + B);
+	// this wave's region: dirty words, chain stacks, target-heading origins (cmode_lds_bytes)
+	uint32_t *dl0 = reinterpret_cast<uint32_t *>(sub + B) +
+			(size_t)wv * (4 * c.W * spw + 64 * (c.maxd + (STAB ? 3 * P : 0)));
 	int *stk0 = reinterpret_cast<int *>(dl0 + (size_t)4 * c.W * spw);
 	float *OE = reinterpret_cast<float *>(stk0 + (size_t)c.maxd * 64) + lane;
 	const int g = lane >> t.log2K, role = lane & (K - 1);
-	const int local = xcd_block() * spw + g; // XCD-aware: neighbouring skeletons' node rows share L2 lines
-	const bool valid = local < count;
+	// XCD-aware block order: neighbouring skeletons' node rows share L2 lines
+	const int local = (xcd_block() * c.wpb + wv) * spw + g;
+	const bool valid = g < spw && local < count;
 	const size_t s = (size_t)first + (valid ? local : 0);
 	int pend = -1;
 	const uint32_t node_bytes = NB32 ? (uint32_t)((size_t)(3 * B + 2 * t.NC) * 12 * t.N * 4) : 0u;
-	CmodeLane<NB32> C{t, c, s, c.node + s, (size_t)t.N, dl0 + g, spw, stk0 + lane, pre, sub, 0, 0x7fffffff, &pend,
-			buf_rsrc(c.node, node_bytes), (uint32_t)s * 4u};
+	CmodeLane<NB32> C{t, c, s, c.node + s, (size_t)t.N, dl0 + (g < spw ? g : 0), spw, stk0 + lane, pre, sub, 0, 0x7fffffff,
+			&pend, buf_rsrc(c.node, node_bytes), (uint32_t)s * 4u};
+#ifdef MBIK_PROF
+	// 0 effector heading reads, 1 swing, 2 twist, 4 dirty pose chains (cycles), 5 chain nodes,
+	// 6 dirty pose reads, 7 total, 8 after-row cleaning, 9 bone-direction recomputes
+	uint64_t pfa[24] = {};
+	C.pf = pfa;
+	uint64_t *pf = pfa;
+#endif
+	MBIK_PROF_T(k0);
 	if (valid)
 		for (int w = role; w < 4 * c.W; w += K) C.dl[spw * w] = c.dirty[(size_t)w * t.N + s];
 	__syncthreads();
@@ -372,6 +412,7 @@ __global__ __launch_bounds__(64) void mbik_cmode_kernel(DevPlan t, CmodeState c,
 			__syncthreads();
 			// The cleaning the reference's first read above the segment root did: the dirty
 			// chain from the recorded node up, one lane at a time (siblings share it).
+			MBIK_PROF_T(r0);
 			uint64_t todo = __ballot(pend >= 0);
 			while (todo) {
 				const int l = __ffsll((unsigned long long)todo) - 1;
@@ -384,6 +425,8 @@ __global__ __launch_bounds__(64) void mbik_cmode_kernel(DevPlan t, CmodeState c,
 				}
 				__threadfence_block();
 			}
+			MBIK_PROF_T(r1);
+			MBIK_PROF_ADD(8, r0, r1);
 			__syncthreads();
 		}
 	}
@@ -403,6 +446,12 @@ __global__ __launch_bounds__(64) void mbik_cmode_kernel(DevPlan t, CmodeState c,
 	__syncthreads();
 	if (valid)
 		for (int w = role; w < 4 * c.W; w += K) c.dirty[(size_t)w * t.N + s] = C.dl[spw * w];
+#ifdef MBIK_PROF
+	MBIK_PROF_T(k1);
+	pfa[7] += k1 - k0;
+	if (valid)
+		for (int i = 0; i < 24; i++) atomicAdd(&g_mbik_prof[i], (unsigned long long)pfa[i]);
+#endif
 }
 
 // A fresh node tree (_bone_list_changed): pose locals = the setup pose, every cache dirty.

@@ -561,6 +561,18 @@ __device__ __forceinline__ void effector_headings(const DevPlan &t, const EffPre
 		// loads during the current product
 		auto walk = [&](int a, int b) {
 			if (a > b) return;
+#ifdef MBIK_WALK2
+			// (A/B: two path bones ahead)
+			X3 Ln = L.ld(t.eff_path[off + a]);
+			X3 Lm = a < b ? L.ld(t.eff_path[off + a + 1]) : Ln;
+			for (int d = a; d < b; d++) {
+				const X3 Lc = Ln;
+				Ln = Lm;
+				if (d + 2 <= b) Lm = L.ld(t.eff_path[off + d + 2]);
+				X = X * Lc;
+			}
+			X = X * Ln;
+#else
 			X3 Ln = L.ld(t.eff_path[off + a]);
 			for (int d = a; d < b; d++) {
 				const X3 Lc = Ln;
@@ -568,6 +580,7 @@ __device__ __forceinline__ void effector_headings(const DevPlan &t, const EffPre
 				X = X * Lc;
 			}
 			X = X * Ln;
+#endif
 		};
 		int d = d0;
 		if (pc) {
@@ -1601,6 +1614,7 @@ struct mbik_plan {
 	// constraint_mode: the persistent IKNode3D caches (cmode.h), lanes per skeleton (0 = auto)
 	CmodeState cm{};
 	int cm_lanes = 0;
+	int cm_spw_div = 0;                                  // constraint_mode: skeletons per wave = (64 / K) >> cm_spw_div
 	// the creation inputs, for mbik_plan_save (the topology is rebuilt from them on load)
 	std::vector<int32_t> src_parents;
 	std::vector<mbik_pin> src_pins;
@@ -1804,10 +1818,29 @@ int ensure_schedule(mbik_plan *p, int64_t nlaunch) {
 // constraint_mode block LDS (cmode.h): topology blob, pre-order tables, the dirty words of
 // the block's 64 / K skeletons, then per lane the chain stack and, with stabilization, the
 // target-heading origins.
+// Per wave: the dirty words of its spw skeletons, and per lane the chain stack and (STAB) the
+// target-heading origins; the topology and pre-order tables once per block.
+static size_t cmode_wave_words(const mbik_plan *p, int spw) {
+	const mbik::HostPlan &h = p->host;
+	return (size_t)spw * 4 * p->cm.W + 64 * ((size_t)p->cm.maxd + (h.stabilization_passes > 0 ? 3 * (size_t)h.P : 0));
+}
 size_t cmode_lds_bytes(const mbik_plan *p) {
 	const mbik::HostPlan &h = p->host;
-	return ((size_t)p->dev.topo_words + 2 * (size_t)h.B + (size_t)(64 >> h.log2K) * 4 * p->cm.W +
-				   64 * ((size_t)p->cm.maxd + (h.stabilization_passes > 0 ? 3 * (size_t)h.P : 0))) * sizeof(float);
+	return ((size_t)p->dev.topo_words + 2 * (size_t)h.B + (size_t)p->cm.wpb * cmode_wave_words(p, p->cm.spw)) * sizeof(float);
+}
+// constraint_mode launch shape: spw skeletons per wave (cm_spw_div halves 64 / K that many
+// times), and as many waves per block (<= kCmodeMaxWaves) as share the block's LDS within
+// 160 KiB and leave the launch with at least one block per CU.
+void cmode_shape(mbik_plan *p, int count) {
+	const mbik::HostPlan &h = p->host;
+	const int full = 64 >> h.log2K;
+	p->cm.spw = p->spw_override > 0 ? std::min(full, p->spw_override) : std::max(1, full >> std::max(0, p->cm_spw_div));
+	int wpb = kCmodeMaxWaves;
+	const size_t fixed = (size_t)p->dev.topo_words + 2 * (size_t)h.B;
+	while (wpb > 1 && ((fixed + (size_t)wpb * cmode_wave_words(p, p->cm.spw)) * sizeof(float) > 160 * 1024 ||
+							  (size_t)(count + (size_t)wpb * p->cm.spw - 1) / ((size_t)wpb * p->cm.spw) < (size_t)p->cu_count))
+		wpb >>= 1;
+	p->cm.wpb = wpb;
 }
 
 // Resets the constraint_mode node caches of skeletons [first, first+count) to a fresh tree
@@ -1950,6 +1983,7 @@ int launch(mbik_plan *p, int first, int count, const float *pose_in, const float
 	int rc = ensure_schedule(p, count);
 	if (rc) return rc;
 	if (h.constraint_mode) {
+		cmode_shape(p, count);
 		const size_t clds = cmode_lds_bytes(p);
 		if (clds > 160 * 1024) return fail(MBIK_EUNSUPPORTED, "skeleton too large for the constraint_mode LDS layout");
 		static std::once_flag conce;
@@ -1963,9 +1997,9 @@ int launch(mbik_plan *p, int first, int count, const float *pose_in, const float
 		const bool nb32 = (size_t)(3 * h.B + 2 * h.NC) * 12 * (size_t)h.N * sizeof(float) < (size_t(1) << 32) && !p->tab64;
 		auto ck = h.stabilization_passes > 0 ? (nb32 ? mbik_cmode_kernel<true, true> : mbik_cmode_kernel<true, false>)
 											 : (nb32 ? mbik_cmode_kernel<false, true> : mbik_cmode_kernel<false, false>);
-		const int cspw = 64 >> h.log2K;
-		hipLaunchKernelGGL(ck, dim3((unsigned)((count + cspw - 1) / cspw)), dim3(64), clds, stream, p->dev, p->cm, first, count,
-				pose_in, targets, pose_out, iterations, seg_lo, seg_hi);
+		const int per_block = p->cm.spw * p->cm.wpb;
+		hipLaunchKernelGGL(ck, dim3((unsigned)((count + per_block - 1) / per_block)), dim3(64 * p->cm.wpb), clds, stream, p->dev,
+				p->cm, first, count, pose_in, targets, pose_out, iterations, seg_lo, seg_hi);
 		hipError_t e = hipGetLastError();
 		if (e != hipSuccess) return fail(MBIK_EHIP, std::string("kernel launch failed: ") + hipGetErrorString(e));
 		return MBIK_OK;
@@ -2399,7 +2433,7 @@ int32_t mbik_plan_create_device_opts(int32_t n_rigs, const mbik_skeleton_desc *d
 // ---- plan serialisation (mbik_plan_save / mbik_plan_load) ----
 namespace {
 constexpr char kPlanMagic[8] = {'M', 'B', 'I', 'K', 'P', 'L', 'A', 'N'};
-constexpr uint32_t kPlanFormat = 3; // 2: + the table-addressing override; 3: + libm_variant (1 and 2 are still read)
+constexpr uint32_t kPlanFormat = 3; // 2: + the table-addressing override; 3: + libm_variant, constraint_mode spw (1 and 2 are still read)
 struct PlanWriter {
 	std::vector<char> b;
 	void bytes(const void *v, size_t n) {
@@ -2481,7 +2515,7 @@ int32_t mbik_plan_save(const mbik_plan *p, void *buf, uint64_t capacity, uint64_
 	w.vec(CF);
 	w.vec(CD);
 	for (int32_t v : {p->lanes_override, p->spw_override, p->interval_override, p->staging_override, p->locals_override,
-				 p->waves_override, p->cm_lanes, p->tab64})
+				 p->waves_override, p->cm_lanes, p->tab64, p->cm_spw_div})
 		w.put<int32_t>(v);
 	std::vector<char> cm;
 	if (h.constraint_mode && N) {
@@ -2529,8 +2563,8 @@ int32_t mbik_plan_load(const void *buf, uint64_t size, int32_t device, mbik_plan
 	const int32_t setup_max_cones = r.get<int32_t>();
 	std::vector<float> D = r.vec<float>(kMax), CF = r.vec<float>(kMax);
 	std::vector<double> CD = r.vec<double>(kMax);
-	int32_t ov[8] = {};
-	for (int i = 0; i < (format >= 2 ? 8 : 7); i++) ov[i] = r.get<int32_t>();
+	int32_t ov[9] = {};
+	for (int i = 0; i < (format >= 3 ? 9 : format == 2 ? 8 : 7); i++) ov[i] = r.get<int32_t>();
 	std::vector<char> cm = r.vec<char>(kMax);
 	const int32_t libm = format >= 3 ? r.get<int32_t>() : MBIK_LIBM_VARIANT_FMA;
 	if (!r.ok || N <= 0) return fail(MBIK_EINVAL, "truncated or corrupt saved plan");
@@ -2569,6 +2603,7 @@ int32_t mbik_plan_load(const void *buf, uint64_t size, int32_t device, mbik_plan
 	p->waves_override = ov[5];
 	p->cm_lanes = ov[6];
 	p->tab64 = ov[7] != 0;
+	p->cm_spw_div = std::max(0, std::min(6, ov[8]));
 	if (h.constraint_mode) {
 		const int W = std::max(1, (h.cm_npos + 31) / 32);
 		const size_t want = (size_t)(3 * h.B + 2 * h.NC) * 12 * n * sizeof(float) + 4 * (size_t)W * n * sizeof(uint32_t);
@@ -2778,9 +2813,14 @@ static int cmode_autotune(mbik_plan *p, int first, int count, const float *pose_
 	}
 	int rc = copy(true);
 	float best_ms = 0.0f;
-	int best = 0;
-	for (int lanes = 1; lanes <= max_lanes && rc == MBIK_OK; lanes *= 2) {
+	int best = 0, best_div = 0;
+	// lanes per skeleton x skeletons per wave (full waves, or half: twice the waves per SIMD
+	// for the node-cache misses to overlap)
+	for (int cand = 0; cand < 2 * 7 && rc == MBIK_OK; cand++) {
+		const int lanes = 1 << (cand >> 1), div = cand & 1;
+		if (lanes > max_lanes) break;
 		p->cm_lanes = lanes;
+		p->cm_spw_div = div;
 		if ((rc = ensure_schedule(p, count)) != MBIK_OK) break;
 		float ms = 0.0f;
 		for (int r = 0; r < 3 && rc == MBIK_OK; r++) { // first run warms up, untimed
@@ -2796,6 +2836,7 @@ static int cmode_autotune(mbik_plan *p, int first, int count, const float *pose_
 		if (rc == MBIK_OK && (best == 0 || ms < best_ms)) {
 			best_ms = ms;
 			best = lanes;
+			best_div = div;
 		}
 	}
 	if (rc == MBIK_OK) rc = copy(false);
@@ -2804,6 +2845,7 @@ static int cmode_autotune(mbik_plan *p, int first, int count, const float *pose_
 	(void)hipEventDestroy(e1);
 	(void)hipFree(save);
 	p->cm_lanes = best;
+	p->cm_spw_div = best_div;
 	if (rc != MBIK_OK) return rc;
 	return ensure_schedule(p, count);
 }

@@ -35,12 +35,14 @@ def animate(pose, rng, angle=0.2):
     return out
 
 
-def run_frames(oracle, wl, frames=4, stab=0, seed=0, lanes=0):
+def run_frames(oracle, wl, frames=4, stab=0, seed=0, lanes=0, spw=0):
     """Frame 1 starts from the setup pose; then the output is fed back (a still skeleton)
     and, every other frame, animated."""
     rng = np.random.default_rng(seed)
     ref_o = oracle.Oracle(wl, constraint_mode=True, stabilization_passes=stab)
     plan = Plan.from_workload(wl, constraint_mode=True, stabilization_passes=stab, lanes=lanes)
+    if spw:
+        plan.set_layout(lanes, spw, 0)
     pose = wl.pose.copy()
     changed = 0
     for f in range(frames):
@@ -154,3 +156,12 @@ def test_autotune_keeps_the_node_caches(oracle, mbik, torch_dev):
 @pytest.mark.parametrize("lanes", [1, 2, 4, 8, 16])
 def test_lane_counts(oracle, mbik, lanes):
     run_frames(oracle, W.generate(5, 6), frames=2, lanes=lanes, seed=60)
+
+
+@pytest.mark.parametrize("cfg,n,lanes,spw,stab", [(2, 3200, 4, 3, 0), (5, 2048, 4, 2, 0), (5, 1024, 2, 1, 2), (2, 700, 1, 64, 0)])
+def test_multiwave_blocks_and_partial_waves(oracle, mbik, cfg, n, lanes, spw, stab):
+    """constraint_mode blocks of several waves sharing one LDS copy of the topology, each wave
+    holding fewer skeletons than 64 / K (cmode_shape: enough blocks for every CU, then as many
+    waves per block as fit): the same bits over animated frames."""
+    wl = W.generate(cfg, n, first=123)
+    run_frames(oracle, wl, frames=3, stab=stab, seed=70 + cfg, lanes=lanes, spw=spw)
