@@ -25,8 +25,21 @@
 // the reference does at the first such read is applied after the row, one lane at a time.
 // Dirty words are shared by the skeleton's lanes: updates are LDS atomics.
 
+// The node state is skeleton-tiled like the default kernel's locals (LocTiled):
+// [N/16][slot][3 quads][16 skeletons][4], element f of node slot k of skeleton s at node_at(),
+// so one node of 16 consecutive skeletons is 768 contiguous bytes and a lane reads its node as
+// three 16-byte quads -- a wave's lane group (consecutive skeletons, one slot) reads 256
+// contiguous bytes per load instruction.  With the plain [slot][12][N] rows (round 2) every
+// element was its own dword load and a 16-skeleton group used half of each 128-B line.
+constexpr int kNodeTile = 16;
+__host__ __device__ __forceinline__ size_t node_at(int slots, size_t s, int k, int f) {
+	return ((s / kNodeTile) * (size_t)slots + (size_t)k) * (12 * kNodeTile) + (size_t)(f >> 2) * (4 * kNodeTile) +
+			(s % kNodeTile) * 4 + (f & 3);
+}
+__host__ __device__ __forceinline__ size_t node_area_floats(int slots, size_t N) { return (N + kNodeTile - 1) / kNodeTile * kNodeTile * (size_t)slots * 12; }
+
 struct CmodeState {
-	float *node;        // [slot][12][N]: pose local (B), pose global (B), bone-direction global (B),
+	float *node;        // node_at(): slots pose local (B), pose global (B), bone-direction global (B),
 	                    // constraint-orientation global (NC), twist global (NC)
 	uint32_t *dirty;    // [kind * W + word][N], kinds: pose, bone direction, orientation, twist
 	const int *pre;     // [B] pre-order position in the pose-node forest (list bones)
@@ -39,17 +52,17 @@ struct CmodeState {
 
 enum { CK_POSE = 0, CK_BDIR = 1, CK_COR = 2, CK_CTW = 3 };
 
-// NB32: the node area is below 4 GiB (the usual case; cmode_node_fits_32), so a node read is a
-// buffer load per element -- the slot's lane offset k * 48 N + 4 s in one VGPR, the element's
-// f * 4 N in the instruction's SGPR offset -- with no per-element address arithmetic; else
+// NB32: the node area and the setup tables are below 4 GiB (the usual case), so a node read is
+// three 16-byte buffer loads off one 32-bit lane offset (the element offsets are immediates)
+// and the setup tables are read with the solve kernel's 32-bit addressing (kTab32); else
 // 64-bit addresses.
 template <bool NB32>
 struct CmodeLane {
 	const DevPlan &t;
 	const CmodeState &c;
 	size_t s;             // absolute skeleton index (plan tables)
-	float *node;          // this skeleton's node state: element f of slot k at node[(12 k + f) * fs]
-	size_t fs;            // element stride of the node state (the plan's N)
+	float *node;          // this skeleton's node state: element f of slot k at node[k * 192 + (f / 4) * 64 + f % 4]
+	int slots;            // node slots per skeleton (3 B + 2 NC)
 	uint32_t *dl;         // this skeleton's dirty words: dl[(kind * W + w) * dls]
 	int dls;              // their interleave (skeletons per block)
 	int *stk;             // this lane's chain stack: stk[i * 64]
@@ -57,23 +70,23 @@ struct CmodeLane {
 	int lo, hi;           // pre-order range this lane may write (its segment root's subtree)
 	int *pend;            // pose node whose dirty chain this lane read privately (-1 none)
 	__amdgpu_buffer_rsrc_t r; // NB32: the whole node area
-	uint32_t s4;          // NB32: 4 s
+	uint32_t nb;          // NB32: byte offset of this skeleton's slot 0, element 0
 #ifdef MBIK_PROF
 	uint64_t *pf;         // diagnostic counters (tools/prof_cmode.py): see mbik_cmode_kernel
 #endif
 
-	__device__ __forceinline__ float *slot(int k) const { return node + (size_t)k * 12 * fs; }
 	__device__ __forceinline__ X3 ld(int k) const {
 		X3 x;
 		float v[12];
 		if constexpr (NB32) {
-			const uint32_t N4 = (uint32_t)fs * 4u, o = (uint32_t)k * 12u * N4 + s4;
+			const uint32_t o = nb + (uint32_t)k * (48u * kNodeTile);
 #pragma unroll
-			for (int f = 0; f < 12; f++) v[f] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, o, (uint32_t)f * N4, 0));
+			for (int f = 0; f < 12; f++)
+				v[f] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, o + 16u * kNodeTile * (f >> 2) + 4u * (f & 3), 0, 0));
 		} else {
-			const float *p = slot(k);
+			const float *p = node + (size_t)k * 12 * kNodeTile;
 #pragma unroll
-			for (int f = 0; f < 12; f++) v[f] = p[(size_t)f * fs];
+			for (int f = 0; f < 12; f++) v[f] = p[(f >> 2) * 4 * kNodeTile + (f & 3)];
 		}
 #pragma unroll
 		for (int i = 0; i < 3; i++) x.b.r[i] = v3(v[3 * i], v[3 * i + 1], v[3 * i + 2]);
@@ -84,13 +97,14 @@ struct CmodeLane {
 		const float v[12] = {x.b.r[0].x, x.b.r[0].y, x.b.r[0].z, x.b.r[1].x, x.b.r[1].y, x.b.r[1].z,
 				x.b.r[2].x, x.b.r[2].y, x.b.r[2].z, x.o.x, x.o.y, x.o.z};
 		if constexpr (NB32) {
-			const uint32_t N4 = (uint32_t)fs * 4u, o = (uint32_t)k * 12u * N4 + s4;
+			const uint32_t o = nb + (uint32_t)k * (48u * kNodeTile);
 #pragma unroll
-			for (int f = 0; f < 12; f++) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v[f]), r, o, (uint32_t)f * N4, 0);
+			for (int f = 0; f < 12; f++)
+				__builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v[f]), r, o + 16u * kNodeTile * (f >> 2) + 4u * (f & 3), 0, 0);
 		} else {
-			float *p = slot(k);
+			float *p = node + (size_t)k * 12 * kNodeTile;
 #pragma unroll
-			for (int f = 0; f < 12; f++) p[(size_t)f * fs] = v[f];
+			for (int f = 0; f < 12; f++) p[(f >> 2) * 4 * kNodeTile + (f & 3)] = v[f];
 		}
 	}
 	__device__ __forceinline__ int LP(int b) const { return b; }
@@ -146,7 +160,8 @@ struct CmodeLane {
 		}
 		// Top-down over stk[n-1] (= x) .. stk[0] (= b).  The chain's locals are known now, so
 		// their loads run two nodes ahead of the products: a chain of n dependent node-cache
-		// misses becomes ~n/3 round trips (the products and their order are unchanged).
+		// misses becomes ~n/3 round trips (the products and their order are unchanged; three
+		// ahead measured 0.5 % slower on C5).
 		const X3 Lx = ld(LP(x));
 		X3 La = n >= 2 ? ld(LP(stk[64 * (n - 2)])) : Lx;
 		X3 Lb = n >= 3 ? ld(LP(stk[64 * (n - 3)])) : Lx;
@@ -182,10 +197,16 @@ struct CmodeLane {
 #ifdef MBIK_PROF
 		pf[9] += 1;
 #endif
-		const X3 G = pose_global(b) * X3{ld_soa_basis(t, t.D, b, 9, 0, s), v3(0, 0, 0)};
+		const X3 G = pose_global(b) * X3{ld_soa_basis<NB32 ? kTab32 : kTab64>(t, t.D, b, 9, 0, s), v3(0, 0, 0)};
 		st(GD(b), G);
 		set_clean(CK_BDIR, b);
 		return G;
+	}
+	// A read whose value is not used (the heading builds' reads in a plain constraint_mode
+	// step only matter for the caches they refresh): the recomputation of a dirty node, no
+	// load of a clean one.
+	__device__ void bdir_touch(int b) const {
+		if (dirty(CK_BDIR, b)) (void)bdir_global(b);
 	}
 	// constraint_orientation_transform: parent = the parent bone's pose node; its local stays
 	// the identity (only set_global_pose copies an origin into it, ik_bone_3d.cpp:145-151).
@@ -203,7 +224,7 @@ struct CmodeLane {
 		const int k = GT(slot_);
 		if (!dirty(CK_CTW, b)) return ld(k);
 		const X3 G = pose_global(t.bone_pose_parent[b]) *
-				X3{ld_soa_basis(t, t.CF, slot_, t.cf_stride, mbik::CF_TWIST_T, s), v3(0, 0, 0)};
+				X3{ld_soa_basis<NB32 ? kTab32 : kTab64>(t, t.CF, slot_, t.cf_stride, mbik::CF_TWIST_T, s), v3(0, 0, 0)};
 		st(k, G);
 		set_clean(CK_CTW, b);
 		return G;
@@ -229,19 +250,21 @@ __device__ void cmode_step(const CmodeLane<NB32> &C, int seg, int k, const float
 	MBIK_PROF_T(c0);
 	for (int i = e0; i < e1; i++) {
 		const int e = t.seg_effs[i];
-		const X3 E = C.bdir_global(t.eff_bone[e]);
 		if (stab) {
+			const X3 E = C.bdir_global(t.eff_bone[e]);
 			OE[ls * (3 * e)] = E.o.x;
 			OE[ls * (3 * e + 1)] = E.o.y;
 			OE[ls * (3 * e + 2)] = E.o.z;
+		} else {
+			C.bdir_touch(t.eff_bone[e]);
 		}
 	}
-	if (e1 > e0) (void)C.bdir_global(b);
+	if (e1 > e0) C.bdir_touch(b);
 	const X3 prev = C.ld(C.LP(b));
 	for (int attempt = 0;; attempt++) {
 		if (attempt > 0 && e1 > e0) { // the retry's tip headings (:141)
-			for (int i = e0; i < e1; i++) (void)C.bdir_global(t.eff_bone[t.seg_effs[i]]);
-			(void)C.bdir_global(b);
+			for (int i = e0; i < e1; i++) C.bdir_touch(t.eff_bone[t.seg_effs[i]]);
+			C.bdir_touch(b);
 		}
 		MBIK_PROF_T(c1);
 		MBIK_PROF_ADD(0, c0, c1);
@@ -253,7 +276,7 @@ __device__ void cmode_step(const CmodeLane<NB32> &C, int seg, int k, const float
 			const V3 p2 = xform(Gd, v3(0.0f, 1.0f, 0.0f));
 			const V3 tip = xform(affine_inverse(Gc), p2);
 			double in_bounds = 1.0;
-			const V3 inl = local_point_in_limits(t, slot_, C.s, tip, in_bounds);
+			const V3 inl = local_point_in_limits<NB32 ? kTab32 : kTab64>(t, slot_, C.s, tip, in_bounds);
 			if (in_bounds < 0) {
 				const V3 cp2 = xform(Gc, inl);
 				const Q rect = arc(p2 - p1, cp2 - p1);
@@ -273,9 +296,10 @@ __device__ void cmode_step(const CmodeLane<NB32> &C, int seg, int k, const float
 			const X3 Gt = C.twist_global(b);
 			const X3 Gs = C.pose_global(b);
 			const B3 pgi = inverse(C.pose_global(t.bone_pose_parent[b]).b);
-			const Q tcr = q4(soa(t, t.CF, slot_, cs, mbik::CF_TWIST_Q, C.s), soa(t, t.CF, slot_, cs, mbik::CF_TWIST_Q + 1, C.s),
-					soa(t, t.CF, slot_, cs, mbik::CF_TWIST_Q + 2, C.s), soa(t, t.CF, slot_, cs, mbik::CF_TWIST_Q + 3, C.s));
-			const float half_cos = soa(t, t.CF, slot_, cs, mbik::CF_TWIST_COS, C.s);
+			constexpr int TA = NB32 ? kTab32 : kTab64;
+			const Q tcr = q4(soa<TA>(t, t.CF, slot_, cs, mbik::CF_TWIST_Q, C.s), soa<TA>(t, t.CF, slot_, cs, mbik::CF_TWIST_Q + 1, C.s),
+					soa<TA>(t, t.CF, slot_, cs, mbik::CF_TWIST_Q + 2, C.s), soa<TA>(t, t.CF, slot_, cs, mbik::CF_TWIST_Q + 3, C.s));
+			const float half_cos = soa<TA>(t, t.CF, slot_, cs, mbik::CF_TWIST_COS, C.s);
 			const B3 gtc = Gt.b * from_quat(tcr);
 			const B3 align = orthonormalized(inverse(gtc) * Gs.b);
 			Q sw, tw;
@@ -372,9 +396,11 @@ __global__ __launch_bounds__(64 * kCmodeMaxWaves) void mbik_cmode_kernel(DevPlan
 	const bool valid = g < spw && local < count;
 	const size_t s = (size_t)first + (valid ? local : 0);
 	int pend = -1;
-	const uint32_t node_bytes = NB32 ? (uint32_t)((size_t)(3 * B + 2 * t.NC) * 12 * t.N * 4) : 0u;
-	CmodeLane<NB32> C{t, c, s, c.node + s, (size_t)t.N, dl0 + (g < spw ? g : 0), spw, stk0 + lane, pre, sub, 0, 0x7fffffff,
-			&pend, buf_rsrc(c.node, node_bytes), (uint32_t)s * 4u};
+	const int slots = 3 * B + 2 * t.NC;
+	const uint32_t node_bytes = NB32 ? (uint32_t)(node_area_floats(slots, (size_t)t.N) * 4) : 0u;
+	const size_t n0 = node_at(slots, s, 0, 0);
+	CmodeLane<NB32> C{t, c, s, c.node + n0, slots, dl0 + (g < spw ? g : 0), spw, stk0 + lane, pre, sub, 0, 0x7fffffff,
+			&pend, buf_rsrc(c.node, node_bytes), (uint32_t)(n0 * 4)};
 #ifdef MBIK_PROF
 	// 0 effector heading reads, 1 swing, 2 twist, 4 dirty pose chains (cycles), 5 chain nodes,
 	// 6 dirty pose reads, 7 total, 8 after-row cleaning, 9 bone-direction recomputes
@@ -464,10 +490,10 @@ __global__ __launch_bounds__(64) void mbik_cmode_reset_kernel(DevPlan t, CmodeSt
 	for (int b = 0; b < t.B; b++) {
 		if (!(t.bone_flags[b] & mbik::BF_IN_LIST)) continue;
 		const X3 L = pose_to_xform(setup_pose + ((size_t)local * t.B + b) * 10);
-		float *p = c.node + (size_t)b * 12 * t.N + s;
+		float *p = c.node + node_at(3 * t.B + 2 * t.NC, s, b, 0);
 		const float v[12] = {L.b.r[0].x, L.b.r[0].y, L.b.r[0].z, L.b.r[1].x, L.b.r[1].y, L.b.r[1].z,
 				L.b.r[2].x, L.b.r[2].y, L.b.r[2].z, L.o.x, L.o.y, L.o.z};
-		for (int f = 0; f < 12; f++) p[(size_t)f * t.N] = v[f];
+		for (int f = 0; f < 12; f++) p[(f >> 2) * 4 * kNodeTile + (f & 3)] = v[f];
 	}
 	for (int w = 0; w < 4 * c.W; w++) c.dirty[(size_t)w * t.N + s] = ~0u;
 }

@@ -1854,6 +1854,26 @@ int cmode_reset(mbik_plan *p, int first, int count, const float *setup_pose, hip
 	return MBIK_OK;
 }
 
+// Plan files keep constraint_mode's node caches in the plain [slot][12][N] order (format 1's);
+// the device holds them skeleton-tiled (node_at).
+size_t cmode_file_node_bytes(const mbik::HostPlan &h) { return (size_t)(3 * h.B + 2 * h.NC) * 12 * (size_t)h.N * sizeof(float); }
+std::vector<float> cmode_nodes_tiled(const mbik::HostPlan &h, const float *plain) {
+	const int slots = 3 * h.B + 2 * h.NC;
+	const size_t N = (size_t)h.N;
+	std::vector<float> t(node_area_floats(slots, N), 0.0f);
+	for (int k = 0; k < slots; k++)
+		for (int f = 0; f < 12; f++)
+			for (size_t s = 0; s < N; s++) t[node_at(slots, s, k, f)] = plain[((size_t)k * 12 + f) * N + s];
+	return t;
+}
+void cmode_nodes_plain(const mbik::HostPlan &h, const float *tiled, float *plain) {
+	const int slots = 3 * h.B + 2 * h.NC;
+	const size_t N = (size_t)h.N;
+	for (int k = 0; k < slots; k++)
+		for (int f = 0; f < 12; f++)
+			for (size_t s = 0; s < N; s++) plain[((size_t)k * 12 + f) * N + s] = tiled[node_at(slots, s, k, f)];
+}
+
 // constraint_mode: allocates the persistent node caches and builds the fresh tree from the
 // host setup poses of mbik_plan_create.
 int cmode_create(mbik_plan *p, const float *setup_pose, const void *saved) {
@@ -1865,7 +1885,7 @@ int cmode_create(mbik_plan *p, const float *setup_pose, const void *saved) {
 	rc = rc ? rc : upload(p, h.cm_sub, c.sub);
 	if (rc) return rc;
 	const size_t N = (size_t)h.N;
-	const size_t node_bytes = (size_t)(3 * h.B + 2 * h.NC) * 12 * N * sizeof(float);
+	const size_t node_bytes = node_area_floats(3 * h.B + 2 * h.NC, N) * sizeof(float);
 	const size_t dirty_bytes = 4 * (size_t)c.W * N * sizeof(uint32_t);
 	void *a = nullptr, *d = nullptr, *sp = nullptr;
 	if (hipMalloc(&a, std::max<size_t>(node_bytes, 4)) != hipSuccess) return fail(MBIK_ENOMEM, "hipMalloc constraint_mode node caches");
@@ -1876,10 +1896,11 @@ int cmode_create(mbik_plan *p, const float *setup_pose, const void *saved) {
 	c.node = static_cast<float *>(a);
 	c.dirty = static_cast<uint32_t *>(d);
 	if (N == 0) return MBIK_OK;
-	if (saved) { // mbik_plan_load: the saved frame-to-frame node caches
+	if (saved) { // mbik_plan_load: the saved frame-to-frame node caches ([slot][12][N] in the file)
 		const char *sv = static_cast<const char *>(saved);
-		if (hipMemcpy(a, sv, node_bytes, hipMemcpyHostToDevice) != hipSuccess ||
-				hipMemcpy(d, sv + node_bytes, dirty_bytes, hipMemcpyHostToDevice) != hipSuccess)
+		const std::vector<float> tiled = cmode_nodes_tiled(h, reinterpret_cast<const float *>(sv));
+		if (hipMemcpy(a, tiled.data(), node_bytes, hipMemcpyHostToDevice) != hipSuccess ||
+				hipMemcpy(d, sv + cmode_file_node_bytes(h), dirty_bytes, hipMemcpyHostToDevice) != hipSuccess)
 			return fail(MBIK_EHIP, "hipMemcpy constraint_mode state");
 		return MBIK_OK;
 	}
@@ -1994,7 +2015,7 @@ int launch(mbik_plan *p, int first, int count, const float *pose_in, const float
 			(void)hipFuncSetAttribute((const void *)mbik_cmode_kernel<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 		});
 		// node caches below 4 GiB: buffer-resource addressing (cmode.h, NB32)
-		const bool nb32 = (size_t)(3 * h.B + 2 * h.NC) * 12 * (size_t)h.N * sizeof(float) < (size_t(1) << 32) && !p->tab64;
+		const bool nb32 = node_area_floats(3 * h.B + 2 * h.NC, (size_t)h.N) * sizeof(float) < (size_t(1) << 32) && tables_fit_32(p);
 		auto ck = h.stabilization_passes > 0 ? (nb32 ? mbik_cmode_kernel<true, true> : mbik_cmode_kernel<true, false>)
 											 : (nb32 ? mbik_cmode_kernel<false, true> : mbik_cmode_kernel<false, false>);
 		const int per_block = p->cm.spw * p->cm.wpb;
@@ -2520,10 +2541,12 @@ int32_t mbik_plan_save(const mbik_plan *p, void *buf, uint64_t capacity, uint64_
 	std::vector<char> cm;
 	if (h.constraint_mode && N) {
 		cm.resize(cmode_state_bytes(p));
-		const size_t node_bytes = (size_t)(3 * h.B + 2 * h.NC) * 12 * N * sizeof(float);
-		if (hipMemcpy(cm.data(), p->cm.node, node_bytes, hipMemcpyDeviceToHost) != hipSuccess ||
+		const size_t node_bytes = cmode_file_node_bytes(h);
+		std::vector<float> tiled(node_area_floats(3 * h.B + 2 * h.NC, N));
+		if (hipMemcpy(tiled.data(), p->cm.node, tiled.size() * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess ||
 				hipMemcpy(cm.data() + node_bytes, p->cm.dirty, cm.size() - node_bytes, hipMemcpyDeviceToHost) != hipSuccess)
 			return fail(MBIK_EHIP, "hipMemcpy constraint_mode state");
+		cmode_nodes_plain(h, tiled.data(), reinterpret_cast<float *>(cm.data()));
 	}
 	w.vec(cm);
 	w.put<int32_t>(h.libm_variant); // format 3
@@ -2794,7 +2817,7 @@ static int cmode_autotune(mbik_plan *p, int first, int count, const float *pose_
 	mbik::build_schedule(h, 0, count, 0, 0, blocks_per_cu, p, p->cu_count);
 	const int max_lanes = h.K;
 	const size_t N = (size_t)h.N;
-	const size_t node_bytes = (size_t)(3 * h.B + 2 * h.NC) * 12 * N * sizeof(float);
+	const size_t node_bytes = node_area_floats(3 * h.B + 2 * h.NC, N) * sizeof(float);
 	const size_t dirty_bytes = 4 * (size_t)p->cm.W * N * sizeof(uint32_t);
 	void *save = nullptr;
 	if (hipMalloc(&save, node_bytes + dirty_bytes) != hipSuccess) return fail(MBIK_ENOMEM, "hipMalloc autotune state copy");
