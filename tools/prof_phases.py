@@ -14,6 +14,7 @@ L = _lib.load()
 L.mbik_debug_prof.argtypes = [C.c_void_p]
 buf = (C.c_ulonglong * 24)()
 for case in sys.argv[1:]:
+    # CFG:N:LANES[:SPW:INTERVAL[:STAGING:PLACEMENT:WAVES]]
     parts = [int(x) for x in case.split(':')]
     cfg, n, lanes = parts[:3]
     spw, interval = (parts[3:5] + [0, 0])[:2] if len(parts) > 3 else (0, 0)
@@ -21,6 +22,11 @@ for case in sys.argv[1:]:
     p = Plan.from_workload(wl, lanes=lanes)
     if spw or interval:
         p.set_layout(lanes, spw, interval)
+    if len(parts) > 5:
+        staging, placement, waves = parts[5:8]
+        p.set_heading_staging(staging)
+        p.set_locals_placement(placement)
+        p.set_waves_per_simd(waves)
     pi = torch.from_numpy(wl.pose).to(dev); tg = torch.from_numpy(wl.targets).to(dev); po = torch.empty_like(pi)
     st = torch.cuda.current_stream(dev).cuda_stream
     p.solve(pi.data_ptr(), tg.data_ptr(), po.data_ptr(), 0, n, st); torch.cuda.synchronize()
