@@ -622,10 +622,12 @@ void build_schedule(HostPlan &p, int32_t lanes, int64_t nlaunch, int32_t spw_ove
 			int m = K >> ceil_log2(cnt);
 			// without staging, the m lanes of a group each solve the whole segment (j 0 of 1):
 			// identical work and identical stores, so no lane waits on another
-			const bool solo = !p.staging && !p.constraint_mode;
 			std::vector<SchedTask> row(K, SchedTask{-1, 0, 1, 0});
-			for (int i = 0; i < cnt; i++)
-				for (int j = 0; j < m; j++) row[i * m + j] = solo ? SchedTask{l[start + i], 0, 1, 0} : SchedTask{l[start + i], j, m, 0};
+			for (int i = 0; i < cnt; i++) {
+				const int sg = l[start + i];
+				const bool solo = !p.constraint_mode && (p.staging == 0 || (p.staging == 2 && !(p.seg_flags[sg] & SF_TRANSLATE)));
+				for (int j = 0; j < m; j++) row[i * m + j] = solo ? SchedTask{sg, 0, 1, 0} : SchedTask{sg, j, m, 0};
+			}
 			p.sched.insert(p.sched.end(), row.begin(), row.end());
 			p.nrows++;
 		}

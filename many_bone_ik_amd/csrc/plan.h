@@ -100,10 +100,11 @@ struct HostPlan {
 	int32_t K = 4, log2K = 2, spw = 16;
 	int64_t lds_block_bytes = 0;
 	// Heading staging of multi-effector segments: split the heading work over the segment's
-	// lanes and exchange terms through LDS (true), or let every lane of the group solve the
-	// segment alone from registers (false: no staging LDS, more skeletons resident per CU,
-	// longer steps for those segments).  Not for constraint_mode (its lanes own tree ranges).
-	bool staging = true;
+	// lanes and exchange terms through LDS (1), or let every lane of the group solve the
+	// segment alone from registers (0: no staging LDS, more skeletons resident per CU,
+	// longer steps for those segments), or stage only the translating root segments -- the
+	// ones with the most effectors (2).  Not for constraint_mode (its lanes own tree ranges).
+	int staging = 1;
 	// Where the per-skeleton solve state lives during a launch: 0 all of it in LDS; 1 the
 	// bone local transforms L in a per-skeleton device-memory area (L2-resident), the rest in
 	// LDS; 2 all of it in device memory (LDS holds only the block's topology copy).  Less LDS

@@ -1753,7 +1753,7 @@ int ensure_schedule(mbik_plan *p, int64_t nlaunch) {
 	mbik::HostPlan &h = p->host;
 	int lanes = p->lanes_override;
 	if (lanes == 0 && h.constraint_mode && p->cm_lanes > 0) lanes = p->cm_lanes;
-	h.staging = p->staging_override != 0;
+	h.staging = p->staging_override < 0 ? 1 : p->staging_override;
 	h.state_hbm = h.constraint_mode ? 0 : std::max(0, p->locals_override);
 	h.waves_per_simd = (p->waves_override == 2 && !h.constraint_mode && h.stabilization_passes == 0) ? 2 : 1;
 	if (h.state_hbm >= 1 && !tables_fit_32(p))
@@ -1794,7 +1794,7 @@ int ensure_schedule(mbik_plan *p, int64_t nlaunch) {
 		p->dev.sg_bytes = (uint32_t)(p->d_state_floats * sizeof(float));
 		p->dev.state_stride = stride;
 	}
-	if (p->sched_K == h.K && p->sched_c == h.g_interval && p->sched_staging == (int)h.staging &&
+	if (p->sched_K == h.K && p->sched_c == h.g_interval && p->sched_staging == h.staging &&
 			p->sched_locals == h.state_hbm && p->d_sched) {
 		p->dev.spw = h.spw;
 		return MBIK_OK;
@@ -1803,7 +1803,7 @@ int ensure_schedule(mbik_plan *p, int64_t nlaunch) {
 	if (rc) return rc;
 	p->sched_K = h.K;
 	p->sched_c = h.g_interval;
-	p->sched_staging = (int)h.staging;
+	p->sched_staging = h.staging;
 	p->sched_locals = h.state_hbm;
 	p->dev.nrows = h.nrows;
 	p->dev.K = h.K;
@@ -2671,7 +2671,7 @@ int32_t mbik_plan_get_info(const mbik_plan *p, mbik_plan_info *o) {
 	o->algorithmic_flops_per_skeleton = p->alg_flops;
 	o->lds_bytes_per_block = h.constraint_mode ? (int64_t)cmode_lds_bytes(p) : p->host.lds_block_bytes;
 	o->checkpoint_interval = h.g_interval;
-	o->heading_staging = h.staging ? 1 : 0;
+	o->heading_staging = h.staging;
 	o->state_placement = h.state_hbm;
 	o->waves_per_simd = h.waves_per_simd;
 	o->constraint_slots = h.NC;
@@ -2728,7 +2728,7 @@ int32_t mbik_plan_set_locals_placement(mbik_plan *p, int32_t placement) {
 
 int32_t mbik_plan_set_heading_staging(mbik_plan *p, int32_t staging) {
 	if (!p) return fail(MBIK_EINVAL, "null plan");
-	if (staging < -1 || staging > 1) return fail(MBIK_EINVAL, "staging must be -1 (automatic), 0 or 1");
+	if (staging < -1 || staging > 2) return fail(MBIK_EINVAL, "staging must be -1 (automatic), 0, 1 or 2");
 	p->staging_override = staging;
 	p->sched_K = -1;
 	return MBIK_OK;
@@ -2909,6 +2909,11 @@ int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const flo
 	// the same bits; only the time differs.
 	// Lane counts: the pinned one, or the widest sibling level and half of it (two sibling
 	// segments per lane: a longer chain, twice the skeletons per wave).
+	// staging 2 (only translating root segments staged) differs from 0 only with such a
+	// segment of several headings
+	bool has_staged_root = false;
+	for (int sg = 0; sg < p->host.NS; sg++)
+		has_staged_root |= (p->host.seg_flags[sg] & mbik::SF_TRANSLATE) && p->host.seg_nh[sg] >= 2;
 	std::vector<int> lane_cands = {lanes};
 	if (lanes == 0 && p->host.K >= 2) lane_cands.push_back(p->host.K / 2);
 	std::vector<std::tuple<int, int, int, int, int, int>> cands; // (spw override, interval, staging, state placement, lanes, waves)
@@ -2922,9 +2927,10 @@ int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const flo
 			// a second wave per SIMD only pays where LDS no longer bounds the blocks per CU
 			if (wv == 2 && lh == 0 && locals0 < 0) continue;
 			p->host.state_hbm = lh;
-			for (int stg : {1, 0}) {
+			for (int stg : {1, 2, 0}) {
 				if (staging0 >= 0 && stg != staging0) continue;
-				p->host.staging = stg != 0;
+				if (stg == 2 && !has_staged_root) continue; // (the same layouts as 0)
+				p->host.staging = stg;
 				// with the whole state in device memory the interval does not change residency, only
 				// the checkpoint writes against the rebuild products (C5: 2 is 0.7 % faster than 1)
 				const std::vector<int> intervals = lh == 2 ? std::vector<int>{1, 2} : std::vector<int>{1, 2, 4, 1 << 20};

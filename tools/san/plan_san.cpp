@@ -42,7 +42,7 @@ int main(int argc, char **argv) {
 			for (int spw : {0, 1, 3, 64}) {
 				mbik::HostPlan q = h;
 				q.state_hbm = (lanes / 2) % 3;
-				q.staging = (lanes & 1) == 0;
+				q.staging = (lanes & 1) == 0 ? 1 : (interval == 2 ? 2 : 0);
 				mbik::build_schedule(q, lanes, c.N, spw, interval);
 				acc += mbik::lds_floats_per_skeleton(q) + mbik::state_floats_per_skeleton(q) + mbik::topology_bytes(q) + q.nrows;
 			}
