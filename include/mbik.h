@@ -105,7 +105,7 @@ typedef struct mbik_plan_info {
 	double algorithmic_flops_per_skeleton; /* SURVEY.md §8(d) per-bone-step formula x bone-steps x iterations */
 	int64_t lds_bytes_per_block;       /* LDS of one launch block (spw skeletons + topology tables) */
 	int32_t checkpoint_interval;       /* iteration-start globals kept every n-th bone (1 << 20: segment roots only) */
-	int32_t heading_staging;           /* mbik_plan_set_heading_staging in effect (0 / 1 / 2) */
+	int32_t heading_staging;           /* mbik_plan_set_heading_staging in effect (0 .. 3) */
 	int32_t state_placement;           /* mbik_plan_set_locals_placement in effect (0 / 1 / 2) */
 	int32_t waves_per_simd;            /* mbik_plan_set_waves_per_simd in effect (1 / 2) */
 	int32_t constraint_slots;          /* slots of mbik_plan_setup_tables' CF / CD (ABI 3) */
@@ -166,7 +166,8 @@ int32_t mbik_plan_set_layout(mbik_plan *plan, int32_t lanes_per_skeleton, int32_
  * segment's group split its effectors' heading builds and stage the QCP terms in LDS.  0:
  * every lane of the group solves the segment alone from registers -- no staging LDS, so
  * more skeletons fit per CU, at a longer step for those segments.  2: only the translating
- * root segments (the ones with the most effectors) are staged.  -1: automatic
+ * root segments (the ones with the most effectors) are staged; 3: only segments with two or
+ * more effectors (whose path walks the lanes split).  -1: automatic
  * (mbik_plan_autotune times them).  Results do not depend on it. */
 int32_t mbik_plan_set_heading_staging(mbik_plan *plan, int32_t staging);
 /* Where the solve keeps its per-skeleton state during a launch: 0 (default) all in LDS;

@@ -625,7 +625,9 @@ void build_schedule(HostPlan &p, int32_t lanes, int64_t nlaunch, int32_t spw_ove
 			std::vector<SchedTask> row(K, SchedTask{-1, 0, 1, 0});
 			for (int i = 0; i < cnt; i++) {
 				const int sg = l[start + i];
-				const bool solo = !p.constraint_mode && (p.staging == 0 || (p.staging == 2 && !(p.seg_flags[sg] & SF_TRANSLATE)));
+				const bool multi = p.seg_eff_off[sg + 1] - p.seg_eff_off[sg] >= 2;
+				const bool staged = p.staging == 1 || (p.staging == 2 && (p.seg_flags[sg] & SF_TRANSLATE)) || (p.staging == 3 && multi);
+				const bool solo = !p.constraint_mode && !staged;
 				for (int j = 0; j < m; j++) row[i * m + j] = solo ? SchedTask{sg, 0, 1, 0} : SchedTask{sg, j, m, 0};
 			}
 			p.sched.insert(p.sched.end(), row.begin(), row.end());

@@ -103,7 +103,9 @@ struct HostPlan {
 	// lanes and exchange terms through LDS (1), or let every lane of the group solve the
 	// segment alone from registers (0: no staging LDS, more skeletons resident per CU,
 	// longer steps for those segments), or stage only the translating root segments -- the
-	// ones with the most effectors (2).  Not for constraint_mode (its lanes own tree ranges).
+	// ones with the most effectors (2), or only segments with two or more effectors, whose
+	// path walks are what the lanes split (3).  Not for constraint_mode (its lanes own tree
+	// ranges).
 	int staging = 1;
 	// Where the per-skeleton solve state lives during a launch: 0 all of it in LDS; 1 the
 	// bone local transforms L in a per-skeleton device-memory area (L2-resident), the rest in

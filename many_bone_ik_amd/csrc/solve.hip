@@ -2728,7 +2728,7 @@ int32_t mbik_plan_set_locals_placement(mbik_plan *p, int32_t placement) {
 
 int32_t mbik_plan_set_heading_staging(mbik_plan *p, int32_t staging) {
 	if (!p) return fail(MBIK_EINVAL, "null plan");
-	if (staging < -1 || staging > 2) return fail(MBIK_EINVAL, "staging must be -1 (automatic), 0, 1 or 2");
+	if (staging < -1 || staging > 3) return fail(MBIK_EINVAL, "staging must be -1 (automatic), 0, 1, 2 or 3");
 	p->staging_override = staging;
 	p->sched_K = -1;
 	return MBIK_OK;
@@ -2911,9 +2911,12 @@ int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const flo
 	// segments per lane: a longer chain, twice the skeletons per wave).
 	// staging 2 (only translating root segments staged) differs from 0 only with such a
 	// segment of several headings
-	bool has_staged_root = false;
-	for (int sg = 0; sg < p->host.NS; sg++)
+	// (3: only segments of two or more effectors)
+	bool has_staged_root = false, has_multi_eff = false;
+	for (int sg = 0; sg < p->host.NS; sg++) {
 		has_staged_root |= (p->host.seg_flags[sg] & mbik::SF_TRANSLATE) && p->host.seg_nh[sg] >= 2;
+		has_multi_eff |= p->host.seg_eff_off[sg + 1] - p->host.seg_eff_off[sg] >= 2;
+	}
 	std::vector<int> lane_cands = {lanes};
 	if (lanes == 0 && p->host.K >= 2) lane_cands.push_back(p->host.K / 2);
 	std::vector<std::tuple<int, int, int, int, int, int>> cands; // (spw override, interval, staging, state placement, lanes, waves)
@@ -2927,9 +2930,10 @@ int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const flo
 			// a second wave per SIMD only pays where LDS no longer bounds the blocks per CU
 			if (wv == 2 && lh == 0 && locals0 < 0) continue;
 			p->host.state_hbm = lh;
-			for (int stg : {1, 2, 0}) {
+			for (int stg : {1, 3, 2, 0}) {
 				if (staging0 >= 0 && stg != staging0) continue;
 				if (stg == 2 && !has_staged_root) continue; // (the same layouts as 0)
+				if (stg == 3 && !has_multi_eff) continue;   // (the same layouts as 0)
 				p->host.staging = stg;
 				// with the whole state in device memory the interval does not change residency, only
 				// the checkpoint writes against the rebuild products (C5: 2 is 0.7 % faster than 1)

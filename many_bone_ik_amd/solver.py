@@ -212,7 +212,7 @@ class Plan:
     def set_heading_staging(self, staging: int = -1):
         """mbik_plan_set_heading_staging: 1 stage multi-effector segments' headings in LDS,
         0 every lane solves such a segment alone, 2 stage only the translating root segments,
-        -1 automatic; results do not depend on it."""
+        3 only segments with two or more effectors, -1 automatic; results do not depend on it."""
         check(self._L.mbik_plan_set_heading_staging(self.h, int(staging)))
 
     def set_locals_placement(self, placement: int = -1):

@@ -98,11 +98,11 @@ def test_autotune_refuses_overlapping_buffers(mbik, constraint_mode):
 @pytest.mark.parametrize("cfg,n", [(2, 48), (3, 48), (4, 16), (5, 6)])
 @pytest.mark.parametrize("stab", [0, 2])
 @pytest.mark.parametrize("lanes", [0, 16])
-@pytest.mark.parametrize("staging", [0, 2])
+@pytest.mark.parametrize("staging", [0, 2, 3])
 def test_unstaged_headings_bitwise_vs_oracle(oracle, mbik, cfg, n, stab, lanes, staging):
     """mbik_plan_set_heading_staging(0): every lane of a multi-effector segment's group solves
     the segment alone (no LDS staging); (2): only the translating root segments are staged;
-    still bitwise equal to the oracle."""
+    (3): only segments with two or more effectors; still bitwise equal to the oracle."""
     wl = W.generate(cfg, n, first=9000)
     ref = oracle.Oracle(wl, stabilization_passes=stab).solve(wl.pose, wl.targets, threads=8)
     plan = Plan.from_workload(wl, stabilization_passes=stab)
@@ -116,12 +116,12 @@ def test_unstaged_headings_bitwise_vs_oracle(oracle, mbik, cfg, n, stab, lanes, 
 def test_staging_argument_check(mbik):
     plan = Plan.from_workload(W.generate(3, 2))
     with pytest.raises(_lib.MbikError):
-        plan.set_heading_staging(3)
+        plan.set_heading_staging(4)
     plan.set_heading_staging(-1)
 
 
 @pytest.mark.parametrize("cfg,n", [(1, 8), (2, 48), (3, 48), (4, 16), (5, 6)])
-@pytest.mark.parametrize("staging", [1, 0, 2])
+@pytest.mark.parametrize("staging", [1, 0, 2, 3])
 @pytest.mark.parametrize("stab", [0, 2])
 @pytest.mark.parametrize("placement", [1, 2])
 def test_state_in_hbm_bitwise_vs_oracle(oracle, mbik, cfg, n, staging, stab, placement):
