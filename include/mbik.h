@@ -50,7 +50,7 @@ extern "C" {
 #define MBIK_EUNSUPPORTED (-4)
 #define MBIK_ENODEV (-5)
 
-#define MBIK_ABI_VERSION 4
+#define MBIK_ABI_VERSION 5
 
 typedef struct mbik_plan mbik_plan;
 typedef struct mbik_group mbik_group;
@@ -112,6 +112,7 @@ typedef struct mbik_plan_info {
 	int32_t cf_stride;                 /* floats per slot of CF = 14 + 31*max_cones (ABI 3) */
 	int32_t cd_stride;                 /* doubles per slot of CD = 2*max_cones (ABI 3) */
 	int32_t libm_variant;              /* mbik_plan_options.libm_variant the plan was created with (ABI 4) */
+	int32_t helper_wave;               /* 1 when the current layout launches with the helper wave (ABI 5) */
 } mbik_plan_info;
 
 /* Which reference host the plan reproduces bit for bit (ABI 4).  Godot's Math::sin/cos(float)
@@ -150,7 +151,8 @@ void mbik_plan_destroy(mbik_plan *plan);
  * buf == NULL stores the needed size in *size; otherwise capacity must be at least that
  * (MBIK_EINVAL).  It reads the device tables back, so the streams using the plan must be
  * idle.  mbik_plan_load rebuilds the plan on `device` from such a buffer; the loaded plan
- * solves bitwise like the saved one.  Format version 1, little-endian, host-independent. */
+ * solves bitwise like the saved one.  Format version 4 (1-3 still load), little-endian,
+ * host-independent. */
 int32_t mbik_plan_save(const mbik_plan *plan, void *buf, uint64_t capacity, uint64_t *size);
 int32_t mbik_plan_load(const void *buf, uint64_t size, int32_t device, mbik_plan **out_plan);
 int32_t mbik_plan_get_info(const mbik_plan *plan, mbik_plan_info *out);
@@ -181,6 +183,15 @@ int32_t mbik_plan_set_locals_placement(mbik_plan *plan, int32_t placement);
  * be resident at once.  -1: automatic (mbik_plan_autotune times both).  Plans with
  * stabilization passes always use 1.  Results do not depend on it. */
 int32_t mbik_plan_set_waves_per_simd(mbik_plan *plan, int32_t waves);
+/* Helper wave: 1 launches two waves per block, on two SIMDs of a CU; the second runs the
+ * global pass and computes each bone-step's parent-side work (the parent's global and its
+ * inverse, the bone's global, the slerp's target side, the bone-direction and twist frames)
+ * one step ahead of the solving wave, which then runs only what depends on the step's fit.
+ * It pays where SIMDs would otherwise idle: launches resident at once with their state in LDS
+ * (a frame of BASELINE configs[1]).  Serves state placement 0 without stabilization; other
+ * layouts ignore it.  0 off, -1 (default) automatic: off until mbik_plan_autotune has timed
+ * it on a fully resident launch.  Results do not depend on it. */
+int32_t mbik_plan_set_helper_wave(mbik_plan *plan, int32_t helper);
 /* How the solve addresses the per-skeleton setup tables (D, CF, CD).  0 (default): with
  * 32-bit offsets from a buffer resource when every table is below 4 GiB, else with 64-bit
  * element indices.  1: always 64-bit indices (state placement 0 only: placements 1 and 2 need

@@ -820,6 +820,143 @@ __device__ __forceinline__ void wave_sync_lds() {
 	asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // diagnostic: a hard ordering point
 #endif
 }
+// ---- Helper wave (HELP, fully resident placement-0 launches) ----
+// A bone-step's parent-side work depends only on the iteration-start state: the parent's global
+// P (a checkpoint, or rebuilt from one through ancestors not yet solved this iteration), the
+// bone's own iteration-start local (only its own step writes it), and per-skeleton constants.
+// A second wave of the block -- on another SIMD of the CU, which a fully resident launch
+// leaves idle -- runs the global pass and computes that work one step ahead into an LDS ring,
+// so the solving wave's chain keeps only what depends on the step's fit:
+//   P, Gb = P * Lb, inverse(P.b), xform(inverse(P.b), -P.o), the slerp's p_to side,
+//   the bone-direction basis (swing), the twist frame gtc = (P.b * T) * R(centre), its inverse
+//   and the twist limit's half cosine (ik_bone_segment_3d.cpp:129-154, ik_kusudama_3d.cpp:117-132).
+// Same operations on the same inputs: the record's values are the bits the solving wave would
+// have computed.  Ring: kHelpSlots records of kHelpF4 float4 per lane, [slot][field][64 lanes];
+// three LDS counters (records produced / consumed, iterations finished) order the two waves.
+constexpr int kHelpF4 = 18, kHelpSlots = 4;
+constexpr int kHelpRingBytes = kHelpSlots * kHelpF4 * 64 * 16 + 16;
+enum HelpField { HF_P = 0, HF_GB = 12, HF_PINV = 24, HF_PNP = 33, HF_STO = 36, HF_HC = 43, HF_DB = 44, HF_GTC = 53, HF_GTCI = 62 };
+__device__ __forceinline__ float hrf(const float4 *r, int i) { return reinterpret_cast<const float *>(r + (i >> 2) * 64)[i & 3]; }
+__device__ __forceinline__ V3 hrv(const float4 *r, int i) { return v3(hrf(r, i), hrf(r, i + 1), hrf(r, i + 2)); }
+__device__ __forceinline__ B3 hrb(const float4 *r, int i) { return B3{{hrv(r, i), hrv(r, i + 3), hrv(r, i + 6)}}; }
+__device__ __forceinline__ X3 hrx(const float4 *r, int i) { return X3{hrb(r, i), hrv(r, i + 9)}; }
+__device__ __forceinline__ void hw_v(float *f, int i, V3 v) { f[i] = v.x; f[i + 1] = v.y; f[i + 2] = v.z; }
+__device__ __forceinline__ void hw_b(float *f, int i, const B3 &b) { hw_v(f, i, b.r[0]); hw_v(f, i + 3, b.r[1]); hw_v(f, i + 6, b.r[2]); }
+// Waits until counter *f reaches v.  Every wait has an exit: after ~2^22 polls (a fraction of
+// a second; a real wait lasts at most a few bone-steps) the wave stops waiting for the rest of
+// the launch and counts itself in g_mbik_help_stuck (the results are then wrong, and the
+// kernel still drains instead of hanging the GPU).
+__device__ unsigned int g_mbik_help_stuck;
+__device__ __forceinline__ void help_wait(int *f, int v, bool &stuck) {
+	if (stuck) return;
+	for (int n = 0; __builtin_amdgcn_readfirstlane(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) < v; n++) {
+		if (n >= (1 << 22)) {
+			stuck = true;
+			if ((threadIdx.x & 63) == 0) atomicAdd(&g_mbik_help_stuck, 1u);
+			return;
+		}
+		__builtin_amdgcn_s_sleep(1);
+	}
+}
+// The solving wave's wait for record v - 1: counters [0] part A and [1] part B in one 64-bit
+// read; b_ready tells whether part B is already there too (then bone_step skips its wait).
+__device__ __forceinline__ void help_wait_ab(int *f, int v, bool &stuck, bool &b_ready) {
+	b_ready = stuck;
+	if (stuck) return;
+	unsigned long long *f2 = reinterpret_cast<unsigned long long *>(f);
+	for (int n = 0;; n++) {
+		const unsigned long long ab = __hip_atomic_load(f2, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+		const int a = __builtin_amdgcn_readfirstlane((int)(uint32_t)ab), b = __builtin_amdgcn_readfirstlane((int)(uint32_t)(ab >> 32));
+		if (a >= v) {
+			b_ready = b >= v;
+			return;
+		}
+		if (n >= (1 << 22)) {
+			stuck = b_ready = true;
+			if ((threadIdx.x & 63) == 0) atomicAdd(&g_mbik_help_stuck, 1u);
+			return;
+		}
+		__builtin_amdgcn_s_sleep(1);
+	}
+}
+__device__ __forceinline__ void help_post(int *f, int v) { __hip_atomic_store(f, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP); }
+// The record of bone-step k (the helper wave), in two parts so that the solving wave can start
+// a step as soon as the bone's global is there: part A (P, Gb: the headings need Gb), part B
+// (the rest, needed from the rotation on).  The per-skeleton table rows a record reads are
+// constants; HelpRows holds them so the helper can issue the loads early.
+struct HelpRows {
+	B3 Db, Tb;
+	Q tcr;
+	float hc;
+};
+template <int TA>
+__device__ __forceinline__ HelpRows help_rows(const DevPlan &t, int k, size_t s) {
+	HelpRows r;
+	const int4 sr = t.step_rec[k];
+	const int b = sr.x & 0xffff;
+	const int flags = sr.z & 0xffff;
+	const int slot = (sr.y >> 16) - 1;
+	r.Db = B3{};
+	r.Tb = B3{};
+	r.tcr = q4(0, 0, 0, 1);
+	r.hc = 0.0f;
+	if (flags & mbik::BF_ORIENT) r.Db = ld_soa_basis<TA>(t, t.D, b, 9, 0, s);
+	if (flags & mbik::BF_AXIAL) {
+		const int cs = t.cf_stride;
+		r.tcr = q4(soa<TA>(t, t.CF, slot, cs, mbik::CF_TWIST_Q, s), soa<TA>(t, t.CF, slot, cs, mbik::CF_TWIST_Q + 1, s),
+				soa<TA>(t, t.CF, slot, cs, mbik::CF_TWIST_Q + 2, s), soa<TA>(t, t.CF, slot, cs, mbik::CF_TWIST_Q + 3, s));
+		r.hc = soa<TA>(t, t.CF, slot, cs, mbik::CF_TWIST_COS, s);
+		r.Tb = ld_soa_basis<TA>(t, t.CF, slot, cs, mbik::CF_TWIST_T, s);
+	}
+	return r;
+}
+__device__ __forceinline__ void hw_store(float4 *rec, const float *f, int f4a, int f4b) {
+	for (int i = f4a; i < f4b; i++) rec[i * 64] = make_float4(f[4 * i], f[4 * i + 1], f[4 * i + 2], f[4 * i + 3]);
+}
+// part A: P and Gb (float4 fields 0-5)
+template <class LV, class FP>
+__device__ __forceinline__ void help_part_a(const DevPlan &t, int k, const LV &L, const FP G, float4 *rec, X3 &P, B3 &Gbb) {
+	const int4 sr = t.step_rec[k];
+	const int b = sr.x & 0xffff;
+	const int flags = sr.z & 0xffff;
+	const bool hasP = (flags & mbik::SR_HAS_POSE_PARENT) != 0;
+	P = xid();
+	if (flags & mbik::SR_PARENT_GLOBAL) {
+		P = ld_x(G + 12 * ((sr.y & 0xffff) - 1));
+		for (int q = (sr.x >> 16) - 2; q > k; q--) P = P * L.ld(t.seg_bones[q]);
+	}
+	const X3 Lb = L.ld(b);
+	const X3 Gb = hasP ? P * Lb : Lb;
+	Gbb = Gb.b;
+	float f[24];
+	hw_b(f, HF_P, P.b);
+	hw_v(f, HF_P + 9, P.o);
+	hw_b(f, HF_GB, Gb.b);
+	hw_v(f, HF_GB + 9, Gb.o);
+	hw_store(rec, f, 0, 6);
+}
+// part B: everything else (float4 fields 6-17)
+__device__ __forceinline__ void help_part_b(const DevPlan &t, int k, const X3 &P, const B3 &Gbb, const HelpRows &rw, float4 *rec) {
+	const int flags = t.step_rec[k].z & 0xffff;
+	const B3 Pinv = inverse(P.b);
+	const SlerpTo sto = slerp_to(Gbb);
+	float f[4 * kHelpF4];
+	hw_b(f, HF_PINV, Pinv);
+	hw_v(f, HF_PNP, xform(Pinv, -P.o));
+	f[HF_STO] = sto.q.x; f[HF_STO + 1] = sto.q.y; f[HF_STO + 2] = sto.q.z; f[HF_STO + 3] = sto.q.w;
+	f[HF_STO + 4] = sto.len[0]; f[HF_STO + 5] = sto.len[1]; f[HF_STO + 6] = sto.len[2];
+	f[HF_HC] = rw.hc;
+	hw_b(f, HF_DB, rw.Db);
+	for (int i = HF_GTC; i < 4 * kHelpF4; i++) f[i] = 0.0f;
+	if (flags & mbik::BF_AXIAL) {
+		const B3 Gct = P.b * rw.Tb;
+		const B3 gtc = Gct * from_quat(rw.tcr);
+		hw_b(f, HF_GTC, gtc);
+		hw_b(f, HF_GTCI, inverse(gtc));
+	}
+	hw_store(rec, f, 6, kHelpF4);
+}
+
 // Staged-heading record (multi-lane segments): the 11 QCP::inner_product terms of one heading
 // pair, as floats -- wc1_a * c2_b (a, b = x, y, z), dot(wc1, c1), dot(c2, c2).
 constexpr int HS_REC = 12;
@@ -834,9 +971,12 @@ __device__ __forceinline__ void qcp_terms(const V3 wc1, const V3 c1, const V3 c2
 // STAB: the plan has stabilization passes (a separate instantiation keeps the retry loop and
 // its LDS staging out of the default kernel).
 // PR: reuse effector path prefixes (PathCk) in multi-effector segments solved from registers.
-template <bool STAB, bool PR, int TA, class LV, class FP, class IP>
+// HELP: the parent-side values come from the helper wave's record hrec (kHelpF4 float4 at
+// stride 64), not from this wave.
+template <bool STAB, bool PR, int TA, bool HELP, class LV, class FP, class IP>
 __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j, int m, size_t s, const LV &L, const FP G, const FP TG,
-		const FP ST, const IP SF, const FP HS, const FP OE, const FP MS, double &prev_dev, const EffPre &pre, bool hoist, bool dbh MBIK_PROF_PARAM) {
+		const FP ST, const IP SF, const FP HS, const FP OE, const FP MS, double &prev_dev, const EffPre &pre, bool hoist, bool dbh,
+		const float4 *hrec, int *hflB, int hseq, bool *hstuck MBIK_PROF_PARAM) {
 	MBIK_PROF_T(pt0);
 #ifdef MBIK_PROF
 	uint64_t pt1 = pt0, pt3 = pt0;
@@ -852,18 +992,29 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 	// The parent's iteration-start global: stored if the parent is a checkpoint, else rebuilt
 	// from the nearest checkpoint above it, with the global pass's own products.
 	X3 P = xid();
-	if (flags & mbik::SR_PARENT_GLOBAL) {
-		P = ld_x(G + 12 * ((sr.y & 0xffff) - 1));
-		for (int q = (sr.x >> 16) - 2; q > k; q--) P = P * L.ld(t.seg_bones[q]); // none when no checkpoint is skipped
+	B3 Pinv;
+	if constexpr (HELP) {
+		// (P, Pinv: read after the wait for the record's part B, below)
+	} else {
+		if (flags & mbik::SR_PARENT_GLOBAL) {
+			P = ld_x(G + 12 * ((sr.y & 0xffff) - 1));
+			for (int q = (sr.x >> 16) - 2; q > k; q--) P = P * L.ld(t.seg_bones[q]); // none when no checkpoint is skipped
+		}
+		Pinv = inverse(P.b);
 	}
-	const B3 Pinv = inverse(P.b);
 	const bool stab = STAB && (t.seg_flags[seg] & mbik::SF_STAB) != 0;
 	const X3 Lprev = L.ld(b); // prev_transform (:136)
 	for (int attempt = 0;; attempt++) {
 	const int oe_mode = stab ? (attempt == 0 ? 1 : 2) : 0;
 	X3 Lb = L.ld(b);
-	const X3 Gb = hasP ? P * Lb : Lb;
-	const SlerpTo sto = slerp_to(Gb.b);
+	X3 Gb;
+	SlerpTo sto;
+	if constexpr (HELP) {
+		Gb = hrx(hrec, HF_GB);
+	} else {
+		Gb = hasP ? P * Lb : Lb;
+		sto = slerp_to(Gb.b);
+	}
 	const bool translate = (t.seg_flags[seg] & mbik::SF_TRANSLATE) != 0;
 	const int e0 = t.seg_eff_off[seg], e1 = t.seg_eff_off[seg + 1];
 	const int nh = t.seg_nh[seg];
@@ -1129,6 +1280,18 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 		MBIK_PROF_ADD(10, ph3, ph4);
 	}
 
+	if constexpr (HELP) {
+		MBIK_PROF_T(hb0);
+		if (hflB) help_wait(hflB, hseq + 1, *hstuck);
+		MBIK_PROF_T(hb1);
+		MBIK_PROF_ADD(19, hb0, hb1);
+		P = hrx(hrec, HF_P);
+		Pinv = hrb(hrec, HF_PINV);
+		sto.q = q4(hrf(hrec, HF_STO), hrf(hrec, HF_STO + 1), hrf(hrec, HF_STO + 2), hrf(hrec, HF_STO + 3));
+		sto.len[0] = hrf(hrec, HF_STO + 4);
+		sto.len[1] = hrf(hrec, HF_STO + 5);
+		sto.len[2] = hrf(hrec, HF_STO + 6);
+	}
 	MBIK_PROF_SET(pt1);
 	MBIK_PROF_ADD(1, pt0, pt1);
 	// ---- damp clamp, slerp(…, 0), rotate, translate, set_global_pose (:144-154) ----
@@ -1149,7 +1312,8 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 	X3 Gn = hasP ? P * Lb : Lb;
 	X3 result = {Gn.b, Gn.o + translation};
 	// affine_inverse(P) with P.basis.inverse() already at hand (same arithmetic)
-	Lb = hasP ? X3{Pinv, xform(Pinv, -P.o)} * result : result;
+	if constexpr (HELP) Lb = hasP ? X3{Pinv, hrv(hrec, HF_PNP)} * result : result;
+	else Lb = hasP ? X3{Pinv, xform(Pinv, -P.o)} * result : result;
 	// set_global_pose propagates through b's subtree: pinned children's stale
 	// bone-direction caches are refreshed from here on.
 	// Every lane of the group holds identical values, so each writes its own copy (same
@@ -1181,7 +1345,8 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 		X3 Gs = P * Lb;
 		GsB = Gs.b;
 		gs_ok = true;
-		Gbd_stale.b = Gs.b * ld_soa_basis<TA>(t, t.D, b, 9, 0, s);
+		if constexpr (HELP) Gbd_stale.b = Gs.b * hrb(hrec, HF_DB);
+		else Gbd_stale.b = Gs.b * ld_soa_basis<TA>(t, t.D, b, 9, 0, s);
 		Gbd_stale.o = Gs.o;
 		X3 Gco = {P.b, xform(P, Lb.o)}; // constraint_orientation: (I, pose local origin) under the parent
 		V3 bdx = xform(Gbd_stale, v3(0.0f, 1.0f, 0.0f));
@@ -1204,17 +1369,26 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 #else
 	if (flags & mbik::BF_AXIAL) {
 #endif
-		const int cs = t.cf_stride;
-		Q tcr = q4(soa<TA>(t, t.CF, slot, cs, mbik::CF_TWIST_Q, s), soa<TA>(t, t.CF, slot, cs, mbik::CF_TWIST_Q + 1, s),
-				soa<TA>(t, t.CF, slot, cs, mbik::CF_TWIST_Q + 2, s), soa<TA>(t, t.CF, slot, cs, mbik::CF_TWIST_Q + 3, s));
-		float half_cos = soa<TA>(t, t.CF, slot, cs, mbik::CF_TWIST_COS, s);
-		B3 Tb = ld_soa_basis<TA>(t, t.CF, slot, cs, mbik::CF_TWIST_T, s);
-		B3 Gct = P.b * Tb;
+		B3 gtc, gtci;
+		float half_cos;
+		if constexpr (HELP) {
+			gtc = hrb(hrec, HF_GTC);
+			gtci = hrb(hrec, HF_GTCI);
+			half_cos = hrf(hrec, HF_HC);
+		} else {
+			const int cs = t.cf_stride;
+			Q tcr = q4(soa<TA>(t, t.CF, slot, cs, mbik::CF_TWIST_Q, s), soa<TA>(t, t.CF, slot, cs, mbik::CF_TWIST_Q + 1, s),
+					soa<TA>(t, t.CF, slot, cs, mbik::CF_TWIST_Q + 2, s), soa<TA>(t, t.CF, slot, cs, mbik::CF_TWIST_Q + 3, s));
+			half_cos = soa<TA>(t, t.CF, slot, cs, mbik::CF_TWIST_COS, s);
+			B3 Tb = ld_soa_basis<TA>(t, t.CF, slot, cs, mbik::CF_TWIST_T, s);
+			B3 Gct = P.b * Tb;
+			gtc = Gct * from_quat(tcr);
+		}
 		X3 Gs;
 		if (gs_ok && !swung) Gs.b = GsB;
 		else Gs.b = P.b * Lb.b;
-		B3 gtc = Gct * from_quat(tcr);
-		B3 align = orthonormalized(inverse(gtc) * Gs.b);
+		if constexpr (!HELP) gtci = inverse(gtc);
+		B3 align = orthonormalized(gtci * Gs.b);
 		Q sw, tw;
 		swing_twist_y(get_rotation_quaternion(align), sw, tw);
 		tw = clamp_cos_half(tw, (double)half_cos);
@@ -1288,6 +1462,33 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 #endif
 }
 
+// The same products for the helper wave, whose global pass is the solving wave's wait at each
+// iteration start: the next bone's index and local load before this bone's product and store.
+template <class LV, class FP>
+__device__ void global_pass_pipelined(const DevPlan &t, int seg, const LV &L, const FP G) {
+	const int kb = t.seg_bone_off[seg], kt = t.seg_bone_off[seg + 1] - 1;
+	int b = t.seg_bones[kt];
+	const int pp = t.bone_pose_parent[b];
+	X3 Gprev = pp >= 0 ? ld_x(G + 12 * t.bone_gslot[pp]) : xid();
+	const bool top_origin = pp == mbik::POSE_PARENT_ORIGIN;
+	X3 Lb = L.ld(b);
+	int gs = t.bone_gslot[b];
+	for (int k = kt; k >= kb; k--) {
+		X3 Ln = Lb;
+		int gn = -1;
+		if (k > kb) {
+			const int bn = t.seg_bones[k - 1];
+			Ln = L.ld(bn);
+			gn = t.bone_gslot[bn];
+		}
+		const X3 Gb = k < kt ? Gprev * Lb : (pp >= 0 ? Gprev * Lb : (top_origin ? xid() * Lb : Lb));
+		if (gs >= 0) st_x(G + 12 * gs, Gb);
+		Gprev = Gb;
+		Lb = Ln;
+		gs = gn;
+	}
+}
+
 // Iteration-start globals of one segment, root -> tip (IKNode3D::get_global_transform).
 template <class LV, class FP>
 __device__ void global_pass(const DevPlan &t, int seg, const LV &L, const FP G) {
@@ -1331,11 +1532,24 @@ __device__ __forceinline__ void write_nonfinite(const DevPlan &t, bool valid, bo
 #define MBIK_WAVES_PER_EU 1
 #endif
 // The solve of one block (blk = the plan-local block index after the XCD remap).
-template <bool STAB, int PL, bool HOIST = true, bool T32 = true>
+// Wave-uniform bone-step count of schedule row r: the longest segment among its tasks (the
+// helper and the solving wave walk the same (row, step) sequence).
+__device__ __forceinline__ int row_steps(const DevPlan &t, int r, int seg_lo, int seg_hi) {
+	int n = 0;
+	for (int i = 0; i < t.K; i++) {
+		const int sg = t.sched[r * t.K + i].x;
+		if (sg >= seg_lo && sg <= seg_hi && sg >= 0) n = max(n, t.seg_bone_off[sg + 1] - t.seg_bone_off[sg]);
+	}
+	return __builtin_amdgcn_readfirstlane(n);
+}
+
+template <bool STAB, int PL, bool HOIST = true, bool T32 = true, bool HELP = false>
 __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int count, const float *__restrict__ pose_in,
 		const float *__restrict__ targets, float *__restrict__ pose_out, int iterations, int seg_lo, int seg_hi) {
+	static_assert(!HELP || (!STAB && PL == 0), "the helper wave serves placement-0 launches without stabilization");
 	extern __shared__ float4 lds4[];
-	const int lane = threadIdx.x;
+	const int lane = HELP ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
+	const int wave = HELP ? (int)(threadIdx.x >> 6) : 0;
 #ifdef MBIK_PROF
 	uint64_t pfa[24] = {};
 	uint64_t *pf = pfa;
@@ -1343,7 +1557,7 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 	MBIK_PROF_T(pk0);
 	{
 		uint4 *dst = reinterpret_cast<uint4 *>(lds4);
-		for (int i = lane; i < (t.topo_words >> 2); i += 64) dst[i] = t.topo_blob[i];
+		for (int i = (int)threadIdx.x; i < (t.topo_words >> 2); i += HELP ? 128 : 64) dst[i] = t.topo_blob[i];
 	}
 	const uint32_t *topo = reinterpret_cast<const uint32_t *>(lds4);
 #define MBIK_REPOINT(T, name) t.name = reinterpret_cast<const T *>(topo + t.o_##name);
@@ -1396,7 +1610,7 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 	constexpr int TA = PL == 2 ? kTabTiled : (T32 ? kTab32 : kTab64); // placement 2 reads the tiled table copy
 	const FP OE = rebind<float>(uplus(SF, P, 16));    // stabilization only: 3 per pin
 	const FP MS = uplus(OE, 3 * P, 32);              // stabilization only: 7 per pin
-	if (valid) {
+	if (valid && wave == 0) {
 		for (int b = role; b < B; b += K)
 			if (t.bone_flags[b] & mbik::BF_IN_LIST) L.st(b, pose_to_xform(pose_in + ((size_t)local * B + b) * 10));
 		for (int e = role; e < P; e += K) {
@@ -1405,9 +1619,102 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 			SF[e] = 0;
 		}
 	}
+	float4 *ring = nullptr;
+	int *hfl = nullptr; // [0] records produced (part A), [1] part B produced, [2] consumed, [3] iterations finished
+	if constexpr (HELP) {
+		ring = reinterpret_cast<float4 *>(lds + (size_t)t.spw * t.lds_stride) + lane;
+		hfl = reinterpret_cast<int *>(reinterpret_cast<float4 *>(lds + (size_t)t.spw * t.lds_stride) + kHelpSlots * kHelpF4 * 64);
+		if (threadIdx.x < 4) hfl[threadIdx.x] = 0;
+	}
 	__syncthreads();
 	MBIK_PROF_T(pk1);
 	MBIK_PROF_ADD(0, pk0, pk1);
+	if constexpr (HELP) {
+		if (wave == 1) {
+			// the helper: per iteration the global pass, then every bone-step's record in the
+			// solving wave's (row, step) order, at most kHelpSlots ahead of it.  The first
+			// record's table rows load before the wait for the iteration's end (they are
+			// per-skeleton constants), so that record costs only its arithmetic.
+			int seq = 0, slot = 0;
+			bool stuck = false;
+			const int4 task0 = t.sched[role];
+			const bool act0 = valid && task0.x >= seg_lo && task0.x <= seg_hi;
+			for (int it = 0; it < iterations; it++) {
+				const HelpRows first_rows = help_rows<kTab32>(t, act0 ? t.seg_bone_off[task0.x] : 0, s);
+				help_wait(hfl + 3, it, stuck);
+				MBIK_PROF_T(hg0);
+				for (int r = t.nrows - 1; r >= 0; r--) {
+					const int4 task = t.sched[r * K + role];
+					if (valid && task.x >= 0 && task.y == 0) global_pass_pipelined(t, task.x, L, G);
+					wave_sync_lds();
+				}
+				MBIK_PROF_T(hg1);
+				MBIK_PROF_ADD(21, hg0, hg1);
+				for (int r = 0; r < t.nrows; r++) {
+					const int4 task = t.sched[r * K + role];
+					const bool act = valid && task.x >= seg_lo && task.x <= seg_hi;
+					const int k0 = act ? t.seg_bone_off[task.x] : 0, k1 = act ? t.seg_bone_off[task.x + 1] : 0;
+					const int nq = row_steps(t, r, seg_lo, seg_hi);
+					for (int q = 0; q < nq; q++, seq++) {
+						const HelpRows rw = (r == 0 && q == 0) ? first_rows : help_rows<kTab32>(t, k0 + q < k1 ? k0 + q : 0, s);
+						help_wait(hfl + 2, seq - kHelpSlots + 1, stuck);
+						float4 *rec = ring + slot * (kHelpF4 * 64);
+						X3 P;
+						B3 Gbb;
+						if (k0 + q < k1) help_part_a(t, k0 + q, L, G, rec, P, Gbb);
+						help_post(hfl, seq + 1);
+#ifdef MBIK_PROF
+						if (r == 0 && q == 0) {
+							MBIK_PROF_T(hg2);
+							MBIK_PROF_ADD(22, hg1, hg2);
+						}
+#endif
+						if (k0 + q < k1) help_part_b(t, k0 + q, P, Gbb, rw, rec);
+						help_post(hfl + 1, seq + 1);
+						slot = slot + 1 == kHelpSlots ? 0 : slot + 1;
+					}
+				}
+			}
+#ifdef MBIK_PROF
+			if (lane == 0)
+				for (int i = 20; i < 24; i++) atomicAdd(&g_mbik_prof[i], (unsigned long long)pfa[i]);
+#endif
+			return;
+		}
+		int seq = 0, slot = 0;
+		bool stuck = false;
+		for (int it = 0; it < iterations; it++) {
+			for (int r = 0; r < t.nrows; r++) {
+				const int4 task = t.sched[r * K + role];
+				const bool act = valid && task.x >= seg_lo && task.x <= seg_hi;
+				const int seg = act ? task.x : 0;
+				const int k0 = act ? t.seg_bone_off[seg] : 0, k1 = act ? t.seg_bone_off[seg + 1] : 0;
+				const int nq = row_steps(t, r, seg_lo, seg_hi);
+				double prev_dev = INFINITY;
+				const int e0 = t.seg_eff_off[seg];
+				EffPre pre;
+				const bool hoist = act && kEffHoist && t.seg_eff_off[seg + 1] - e0 == 1 && (task.z == 1 || t.seg_nh[seg] == 1);
+				if (hoist) load_eff<kTab32>(t, t.seg_effs[e0], TG, s, t.seg_hw + t.seg_hw_off[seg] + t.seg_eff_hoff[e0], pre);
+				for (int q = 0; q < nq; q++, seq++) {
+					MBIK_PROF_T(hw0);
+					bool b_ready;
+					help_wait_ab(hfl, seq + 1, stuck, b_ready);
+					MBIK_PROF_T(hw1);
+					MBIK_PROF_ADD(18, hw0, hw1);
+#ifdef MBIK_PROF
+					if (r == 0 && q == 0) MBIK_PROF_ADD(20, hw0, hw1);
+#endif
+					if (k0 + q < k1)
+						bone_step<false, kPathReuse, kTab32, true>(t, seg, k0 + q, task.y, task.z, s, L, G, TG, ST, SF, HS, OE, MS, prev_dev,
+								pre, hoist, false, ring + slot * (kHelpF4 * 64), b_ready ? nullptr : hfl + 1, seq, &stuck MBIK_PROF_ARG);
+					help_post(hfl + 2, seq + 1);
+					slot = slot + 1 == kHelpSlots ? 0 : slot + 1;
+				}
+				wave_sync_lds();
+			}
+			help_post(hfl + 3, it + 1);
+		}
+	} else
 	for (int it = 0; it < iterations; it++) {
 		MBIK_PROF_T(pg0);
 		for (int r = t.nrows - 1; r >= 0; r--) {
@@ -1434,7 +1741,8 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 				const bool dbh = kDbh && !HOIST && !STAB && t.seg_eff_off[seg + 1] - e0 == 1;
 				if (dbh) pre.Db = ld_soa_basis<TA>(t, t.D, t.eff_bone[t.seg_effs[e0]], 9, 0, s);
 				for (int k = t.seg_bone_off[seg]; k < t.seg_bone_off[seg + 1]; k++)
-					bone_step<STAB, kPathReuse && (HOIST || (PL == 2 && !kNoPrPl2) || kPathReuse2W), TA>(t, seg, k, task.y, task.z, s, L, G, TG, ST, SF, HS, OE, MS, prev_dev, pre, hoist, dbh MBIK_PROF_ARG);
+					bone_step<STAB, kPathReuse && (HOIST || (PL == 2 && !kNoPrPl2) || kPathReuse2W), TA, false>(t, seg, k, task.y, task.z, s, L, G, TG, ST, SF, HS, OE, MS, prev_dev, pre, hoist, dbh,
+							nullptr, nullptr, 0, nullptr MBIK_PROF_ARG);
 			}
 			__syncthreads();
 		}
@@ -1483,6 +1791,14 @@ template <bool STAB, int PL, int WPE = MBIK_WAVES_PER_EU, bool T32 = true>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void mbik_solve_kernel(DevPlan t, int first, int count, const float *__restrict__ pose_in,
 		const float *__restrict__ targets, float *__restrict__ pose_out, int iterations, int seg_lo, int seg_hi) {
 	solve_block<STAB, PL, WPE == 1, T32>(t, xcd_block(), first, count, pose_in, targets, pose_out, iterations, seg_lo, seg_hi);
+}
+
+// The same with a helper wave (two waves per block, on two SIMDs of a CU): placement 0, no
+// stabilization, 32-bit table addressing (mbik_plan_set_helper_wave; autotune decides).
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(1, 1))) void mbik_solve_help_kernel(DevPlan t, int first, int count,
+		const float *__restrict__ pose_in, const float *__restrict__ targets, float *__restrict__ pose_out, int iterations, int seg_lo,
+		int seg_hi) {
+	solve_block<false, 0, true, true, true>(t, xcd_block(), first, count, pose_in, targets, pose_out, iterations, seg_lo, seg_hi);
 }
 
 // A heterogeneous batch (mbik_group_solve): several plans -- distinct rigs -- in one launch.
@@ -1600,6 +1916,7 @@ struct mbik_plan {
 	int tab64 = 0;                                       // mbik_plan_set_table_addressing
 	int locals_override = -1;                            // mbik_plan_set_locals_placement; -1 = automatic
 	int waves_override = -1;                             // mbik_plan_set_waves_per_simd; -1 = automatic
+	int helper_override = -1;                            // mbik_plan_set_helper_wave; -1 = automatic
 	int sched_locals = -1;
 	float *d_locals = nullptr;                           // [N][B][12] for state_hbm 1
 	float *d_state = nullptr;                            // [N][state stride] for state_hbm 2
@@ -1732,6 +2049,17 @@ SolveKernel solve_kernel_for(const mbik_plan *p) {
 	if (pl == 0 && !tables_fit_32(p)) return two ? k64[2] : k64[h.stabilization_passes > 0 ? 1 : 0];
 	if (two) return k2[pl];
 	return ks[h.stabilization_passes > 0 ? 1 : 0][pl];
+}
+
+// Whether a launch of the plan's current layout runs with the helper wave
+// (mbik_solve_help_kernel): asked for, and a layout it serves -- state in LDS, no
+// stabilization, one wave per SIMD, 32-bit tables -- whose block LDS still fits with the ring.
+bool helper_on(const mbik_plan *p) {
+	const mbik::HostPlan &h = p->host;
+	if (p->helper_override != 1) return false;
+	if (h.state_hbm != 0 || h.stabilization_passes != 0 || h.waves_per_simd != 1 || h.constraint_mode || !tables_fit_32(p)) return false;
+	const size_t lds = ((size_t)h.spw * p->dev.lds_stride + p->dev.topo_words) * sizeof(float) + kHelpRingBytes;
+	return lds <= 160 * 1024;
 }
 
 // Resident one-wave blocks per CU for a block's LDS size, from the runtime's occupancy
@@ -2032,6 +2360,16 @@ int launch(mbik_plan *p, int first, int count, const float *pose_in, const float
 	if (lds > 160 * 1024) return fail(MBIK_EUNSUPPORTED, "skeleton too large for LDS at this lane count");
 	unsigned blocks = (unsigned)((count + h.spw - 1) / h.spw);
 	auto kern = solve_kernel_for(p);
+	unsigned threads = 64;
+	if (helper_on(p)) {
+		static std::once_flag honce;
+		std::call_once(honce, [] {
+			(void)hipFuncSetAttribute((const void *)mbik_solve_help_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+		});
+		kern = mbik_solve_help_kernel;
+		lds += kHelpRingBytes;
+		threads = 128;
+	}
 	DevPlan d = p->dev;
 	if (h.state_hbm == 2) {
 		if ((rc = ensure_tiled_rows(p, stream)) != MBIK_OK) return rc;
@@ -2041,7 +2379,7 @@ int launch(mbik_plan *p, int first, int count, const float *pose_in, const float
 		d.CD = p->d_CDt;
 		d.row_n = (h.N + kRowTile - 1) / kRowTile * kRowTile;
 	}
-	hipLaunchKernelGGL(kern, dim3(blocks), dim3(64), lds, stream, d, first, count, pose_in, targets, pose_out,
+	hipLaunchKernelGGL(kern, dim3(blocks), dim3(threads), lds, stream, d, first, count, pose_in, targets, pose_out,
 			iterations, seg_lo, seg_hi);
 	hipError_t e = hipGetLastError();
 	if (e != hipSuccess) return fail(MBIK_EHIP, std::string("kernel launch failed: ") + hipGetErrorString(e));
@@ -2454,7 +2792,7 @@ int32_t mbik_plan_create_device_opts(int32_t n_rigs, const mbik_skeleton_desc *d
 // ---- plan serialisation (mbik_plan_save / mbik_plan_load) ----
 namespace {
 constexpr char kPlanMagic[8] = {'M', 'B', 'I', 'K', 'P', 'L', 'A', 'N'};
-constexpr uint32_t kPlanFormat = 3; // 2: + the table-addressing override; 3: + libm_variant, constraint_mode spw (1 and 2 are still read)
+constexpr uint32_t kPlanFormat = 4; // 2: + the table-addressing override; 3: + libm_variant, constraint_mode spw; 4: + the helper-wave override (1-3 are still read)
 struct PlanWriter {
 	std::vector<char> b;
 	void bytes(const void *v, size_t n) {
@@ -2550,6 +2888,7 @@ int32_t mbik_plan_save(const mbik_plan *p, void *buf, uint64_t capacity, uint64_
 	}
 	w.vec(cm);
 	w.put<int32_t>(h.libm_variant); // format 3
+	w.put<int32_t>(p->helper_override); // format 4
 	*size = w.b.size();
 	if (!buf) return MBIK_OK;
 	if (capacity < w.b.size()) return fail(MBIK_EINVAL, "buffer smaller than the saved plan (see *size)");
@@ -2590,8 +2929,10 @@ int32_t mbik_plan_load(const void *buf, uint64_t size, int32_t device, mbik_plan
 	for (int i = 0; i < (format >= 3 ? 9 : format == 2 ? 8 : 7); i++) ov[i] = r.get<int32_t>();
 	std::vector<char> cm = r.vec<char>(kMax);
 	const int32_t libm = format >= 3 ? r.get<int32_t>() : MBIK_LIBM_VARIANT_FMA;
+	const int32_t helper = format >= 4 ? r.get<int32_t>() : -1;
 	if (!r.ok || N <= 0) return fail(MBIK_EINVAL, "truncated or corrupt saved plan");
 	if (libm != MBIK_LIBM_VARIANT_FMA && libm != MBIK_LIBM_VARIANT_SSE2) return fail(MBIK_EINVAL, "saved plan: unknown libm_variant");
+	if (helper < -1 || helper > 1) return fail(MBIK_EINVAL, "saved plan: unknown helper-wave setting");
 	mbik_skeleton_desc desc{};
 	desc.bone_count = (int32_t)p->src_parents.size();
 	desc.parents = p->src_parents.data();
@@ -2627,6 +2968,7 @@ int32_t mbik_plan_load(const void *buf, uint64_t size, int32_t device, mbik_plan
 	p->cm_lanes = ov[6];
 	p->tab64 = ov[7] != 0;
 	p->cm_spw_div = std::max(0, std::min(6, ov[8]));
+	p->helper_override = helper;
 	if (h.constraint_mode) {
 		const int W = std::max(1, (h.cm_npos + 31) / 32);
 		const size_t want = (size_t)(3 * h.B + 2 * h.NC) * 12 * n * sizeof(float) + 4 * (size_t)W * n * sizeof(uint32_t);
@@ -2678,6 +3020,7 @@ int32_t mbik_plan_get_info(const mbik_plan *p, mbik_plan_info *o) {
 	o->cf_stride = h.cf_stride();
 	o->cd_stride = h.cd_stride();
 	o->libm_variant = h.libm_variant;
+	o->helper_wave = helper_on(p) ? 1 : 0;
 	return MBIK_OK;
 }
 
@@ -2706,6 +3049,13 @@ int32_t mbik_plan_set_waves_per_simd(mbik_plan *p, int32_t waves) {
 	if (waves != -1 && waves != 1 && waves != 2) return fail(MBIK_EINVAL, "waves_per_simd must be -1 (automatic), 1 or 2");
 	p->waves_override = waves;
 	p->sched_K = -1;
+	return MBIK_OK;
+}
+
+int32_t mbik_plan_set_helper_wave(mbik_plan *p, int32_t helper) {
+	if (!p) return fail(MBIK_EINVAL, "null plan");
+	if (helper < -1 || helper > 1) return fail(MBIK_EINVAL, "helper wave must be -1 (automatic), 0 (off) or 1 (on)");
+	p->helper_override = helper;
 	return MBIK_OK;
 }
 
@@ -2873,6 +3223,38 @@ static int cmode_autotune(mbik_plan *p, int first, int count, const float *pose_
 	return ensure_schedule(p, count);
 }
 
+// A fully resident launch (the layout is fixed): with the helper wave left automatic, time the
+// launch without and with it and keep the helper only if it is faster beyond the near-tie margin.
+// The helper's second wave needs a free SIMD: at most two blocks of it per CU.
+static int autotune_helper(mbik_plan *p, int first, int count, const float *pose_in, const float *targets, float *pose_out,
+		hipStream_t st) {
+	if (p->helper_override != -1) return MBIK_OK;
+	p->helper_override = 1;
+	const int64_t blocks = (count + p->host.spw - 1) / p->host.spw;
+	if (!helper_on(p) || blocks > 2 * (int64_t)p->cu_count) {
+		p->helper_override = 0;
+		return MBIK_OK;
+	}
+	hipEvent_t e0, e1;
+	if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return fail(MBIK_EHIP, "hipEventCreate");
+	float ms[2] = {0.0f, 0.0f};
+	int rc = MBIK_OK;
+	for (int h = 0; h < 2 && rc == MBIK_OK; h++) {
+		p->helper_override = h;
+		if ((rc = launch(p, first, count, pose_in, targets, pose_out, st, p->host.iterations, 0, p->host.NS - 1)) != MBIK_OK) break;
+		(void)hipEventRecord(e0, st);
+		for (int r = 0; r < 3 && rc == MBIK_OK; r++)
+			rc = launch(p, first, count, pose_in, targets, pose_out, st, p->host.iterations, 0, p->host.NS - 1);
+		(void)hipEventRecord(e1, st);
+		if (rc == MBIK_OK && hipEventSynchronize(e1) != hipSuccess) rc = fail(MBIK_EHIP, "hipEventSynchronize");
+		(void)hipEventElapsedTime(&ms[h], e0, e1);
+	}
+	(void)hipEventDestroy(e0);
+	(void)hipEventDestroy(e1);
+	p->helper_override = rc == MBIK_OK && ms[1] * 1.015f < ms[0] ? 1 : 0;
+	return rc;
+}
+
 int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const float *pose_in, const float *targets,
 		float *pose_out, void *hip_stream) {
 	if (!p) return fail(MBIK_EINVAL, "null plan");
@@ -2902,7 +3284,7 @@ int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const flo
 		int rc0 = ensure_schedule(p, count);
 		if (rc0 != MBIK_OK) return rc0;
 		if ((int64_t)blocks_per_cu(p, p->host.lds_block_bytes) * p->host.spw * p->cu_count >= count && p->host.g_interval == 1)
-			return MBIK_OK;
+			return autotune_helper(p, first, count, pose_in, targets, pose_out, st);
 	}
 	// Candidate layouts: for each heading-staging mode and checkpoint interval, the largest
 	// skeletons-per-block at each distinct residency (blocks per CU).  Every layout computes

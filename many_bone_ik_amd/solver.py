@@ -224,6 +224,12 @@ class Plan:
         """mbik_plan_set_waves_per_simd: 1 or 2 waves per SIMD, -1 automatic."""
         check(self._L.mbik_plan_set_waves_per_simd(self.h, int(waves)))
 
+    def set_helper_wave(self, helper: int = -1):
+        """mbik_plan_set_helper_wave: 1 a second wave per block computes each bone-step's
+        parent-side work one step ahead (fully resident placement-0 launches), 0 off,
+        -1 automatic."""
+        check(self._L.mbik_plan_set_helper_wave(self.h, int(helper)))
+
     def set_table_addressing(self, wide: int = 0):
         """mbik_plan_set_table_addressing: 0 automatic (32-bit offsets below 4 GiB), 1 64-bit indices."""
         check(self._L.mbik_plan_set_table_addressing(self.h, int(wide)))

@@ -1,14 +1,14 @@
 """Per-phase cycle accounting of the solve kernel (needs a -DMBIK_PROF build named by
 MBIK_LIB_OVERRIDE, see tools/prof_build.sh).  Prints, per config, the share of wave
 cycles spent in each phase (summed over waves; one solve launch)."""
-import ctypes as C, json, sys
+import ctypes as C, json, os, sys
 import torch
 sys.path.insert(0, '.')
 from many_bone_ik_amd import _lib, workloads as W
 from many_bone_ik_amd.solver import Plan
 
 NAMES = ["load", "headings_qcp", "clamp_slerp_rotate", "swing", "twist", "global_pass", "store", "total",
-         "step_start", "eff_headings", "qcp_adjugate", "convert_clamp", "slerp", "translate_steps", "qcp_centroid_sums", "tr_headings_build", "tr_staged_sums", "tr_rotate"]
+         "step_start", "eff_headings", "qcp_adjugate", "convert_clamp", "slerp", "translate_steps", "qcp_centroid_sums", "tr_headings_build", "tr_staged_sums", "tr_rotate", "help_wait", "help_wait_b", "help_wait_first", "helper_global_pass", "helper_first_record"]
 dev = torch.device('cuda', 0)
 L = _lib.load()
 L.mbik_debug_prof.argtypes = [C.c_void_p]
@@ -27,6 +27,8 @@ for case in sys.argv[1:]:
         p.set_heading_staging(staging)
         p.set_locals_placement(placement)
         p.set_waves_per_simd(waves)
+    if os.environ.get("MBIK_HELP"):
+        p.set_helper_wave(int(os.environ["MBIK_HELP"]))
     pi = torch.from_numpy(wl.pose).to(dev); tg = torch.from_numpy(wl.targets).to(dev); po = torch.empty_like(pi)
     st = torch.cuda.current_stream(dev).cuda_stream
     p.solve(pi.data_ptr(), tg.data_ptr(), po.data_ptr(), 0, n, st); torch.cuda.synchronize()
