@@ -21,7 +21,9 @@ classes["OTHER_mov_cmp_cndmask_bitwise"] = valu - sum(classes.values())
 wave_cycles = 4 * m["SQ_WAVE_CYCLES"]
 entry = {
     "source": f"tools/valu_mix.sh (3 rocprofv3 --pmc passes of bench.py, layout {key}), per wave, mean over the "
-              "solve dispatches; SQ_WAVE_CYCLES is in 4-cycle units",
+              "solve dispatches; SQ_WAVE_CYCLES is in 4-cycle units"
+              + ("; helper-wave layout: two waves per block (the solving wave and its helper), so every per-wave "
+                 "value is the mean of the two" if key.endswith("_h1") else ""),
     "valu_insts_per_wave": valu,
     "wave_cycles": wave_cycles,
     "valu_issue_floor_cycles": 4 * valu,

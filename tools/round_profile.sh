@@ -12,7 +12,7 @@ export TMPDIR=/tmp
 B="$ROOT/bench.py --config $CFG --steps 20 --warmup 3 --no-cpu-baseline --no-parity"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/ktrace -o run --output-format csv -- python3 $B > $OUT/ktrace.json 2> $OUT/ktrace.log
 # the PMC passes and the final bench line run the layout the kernel-trace run's autotune picked
-LAYOUT=$(python3 -c "import json; c=json.loads(open('$OUT/ktrace.json').read().strip().splitlines()[-1])['config']; l=c['layout']; print(':'.join(str(x) for x in (c['lanes_per_skeleton'], c['skeletons_per_block'], l['checkpoint_interval'], l['heading_staging'], l['state_placement'], l['waves_per_simd'])))")
+LAYOUT=$(python3 -c "import json; c=json.loads(open('$OUT/ktrace.json').read().strip().splitlines()[-1])['config']; l=c['layout']; print(':'.join(str(x) for x in (c['lanes_per_skeleton'], c['skeletons_per_block'], l['checkpoint_interval'], l['heading_staging'], l['state_placement'], l['waves_per_simd'], l.get('helper_wave', 0))))")
 B="$B --layout $LAYOUT"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o run --output-format csv -- python3 $B > $OUT/fetch.json 2> $OUT/fetch.log
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o run --output-format csv -- python3 $B > $OUT/write.json 2> $OUT/write.log
