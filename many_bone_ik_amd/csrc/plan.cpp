@@ -616,6 +616,7 @@ void build_schedule(HostPlan &p, int32_t lanes, int64_t nlaunch, int32_t spw_ove
 	p.log2K = ceil_log2(K);
 	p.sched.clear();
 	p.nrows = 0;
+	p.has_xs = false;
 	for (auto &l : lev) {
 		for (size_t start = 0; start < l.size(); start += K) {
 			int cnt = (int)std::min<size_t>(K, l.size() - start);
@@ -626,9 +627,16 @@ void build_schedule(HostPlan &p, int32_t lanes, int64_t nlaunch, int32_t spw_ove
 			for (int i = 0; i < cnt; i++) {
 				const int sg = l[start + i];
 				const bool multi = p.seg_eff_off[sg + 1] - p.seg_eff_off[sg] >= 2;
-				const bool staged = p.staging == 1 || (p.staging == 2 && (p.seg_flags[sg] & SF_TRANSLATE)) || (p.staging == 3 && multi);
+				const bool tr = (p.seg_flags[sg] & SF_TRANSLATE) != 0;
+				const bool staged = p.staging == 1 || (p.staging == 2 && tr) || (p.staging == 3 && multi) || (p.staging == 5 && tr && multi);
 				const bool solo = !p.constraint_mode && !staged;
-				for (int j = 0; j < m; j++) row[i * m + j] = solo ? SchedTask{sg, 0, 1, 0} : SchedTask{sg, j, m, 0};
+				// staging 4 / 5: multi-effector segments not staged in memory split their effectors
+				// over the group's lanes and exchange the headings lane to lane
+				// (the two-waves-per-SIMD build is the one that serves them; one wave: solo)
+				const bool xs = solo && multi && m >= 2 && (p.staging == 4 || p.staging == 5) && p.waves_per_simd == 2;
+				for (int j = 0; j < m; j++)
+					row[i * m + j] = xs ? SchedTask{sg, j, m, 1} : (solo ? SchedTask{sg, 0, 1, 0} : SchedTask{sg, j, m, 0});
+				p.has_xs |= xs;
 			}
 			p.sched.insert(p.sched.end(), row.begin(), row.end());
 			p.nrows++;
@@ -643,7 +651,7 @@ void build_schedule(HostPlan &p, int32_t lanes, int64_t nlaunch, int32_t spw_ove
 		int used = 0;
 		for (int l = 0; l < K; l++) {
 			const SchedTask &tk = p.sched[(size_t)r * K + l];
-			if (tk.seg < 0 || tk.j != 0 || tk.m < 2 || p.seg_nh[tk.seg] < 2) continue;
+			if (tk.seg < 0 || tk.j != 0 || tk.m < 2 || tk.xs || p.seg_nh[tk.seg] < 2) continue;
 			p.seg_hbase[tk.seg] = used;
 			used += 12 * p.seg_nh[tk.seg] + 24;
 		}

@@ -58,7 +58,8 @@ struct SchedTask {
 	int32_t seg;  // -1 idle
 	int32_t j;    // index of this lane inside the segment's lane group
 	int32_t m;    // lanes in the group (power of two, aligned)
-	int32_t pad;
+	int32_t xs;   // 1: split-exchange (staging 4/5): the group's lanes build alternate effectors' headings and
+	              // share them through cross-lane reads; every lane sums them all in order (no staging memory)
 };
 
 struct HostPlan {
@@ -104,9 +105,14 @@ struct HostPlan {
 	// segment alone from registers (0: no staging LDS, more skeletons resident per CU,
 	// longer steps for those segments), or stage only the translating root segments -- the
 	// ones with the most effectors (2), or only segments with two or more effectors, whose
-	// path walks are what the lanes split (3).  Not for constraint_mode (its lanes own tree
+	// path walks are what the lanes split (3).  4: no segment is staged in memory; the lanes of
+	// a multi-effector segment's group build alternate effectors' headings and read each
+	// other's through cross-lane operations, every lane summing all of them in order (the split
+	// of 1 and 3 without the memory round trips); 5: translating root segments staged as in 2,
+	// the other multi-effector segments as in 4.  Not for constraint_mode (its lanes own tree
 	// ranges).
 	int staging = 1;
+	bool has_xs = false; // the schedule has split-exchange tasks (staging 4 / 5, two-wave build only)
 	// Where the per-skeleton solve state lives during a launch: 0 all of it in LDS; 1 the
 	// bone local transforms L in a per-skeleton device-memory area (L2-resident), the rest in
 	// LDS; 2 all of it in device memory (LDS holds only the block's topology copy).  Less LDS

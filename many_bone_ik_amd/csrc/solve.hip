@@ -525,6 +525,24 @@ __device__ __forceinline__ void load_eff(const DevPlan &t, int e, const FP TG, s
 	}
 }
 __device__ __forceinline__ void heading_terms(const EffPre &p, const X3 &E, V3 oe, V3 ob, Headings &H);
+// The weights and slot mask heading_terms gives effector e's headings (from its priorities and
+// its QCP heading weights hw), without building the headings.
+__device__ __forceinline__ void heading_weights(const DevPlan &t, int e, const double *hw, Headings &H) {
+	H.w[0] = hw[0];
+	H.mask = 1;
+	int k = 1;
+#pragma unroll
+	for (int a = 0; a < 3; a++) {
+		if (t.eff_prio[3 * e + a] > 0.0f) {
+			H.w[1 + 2 * a] = hw[k];
+			H.w[2 + 2 * a] = hw[k + 1];
+			k += 2;
+			H.mask |= 6 << (2 * a);
+		} else {
+			H.w[1 + 2 * a] = H.w[2 + 2 * a] = 0.0;
+		}
+	}
+}
 // oe_mode (stabilization, ik_bone_segment_3d.cpp:135-176): 0 plain; 1 also record the target
 // headings' origin in OE; 2 take that origin from OE (target headings are built once per
 // bone-step, before the retry loop, while tip headings are rebuilt on every pass).
@@ -972,9 +990,10 @@ __device__ __forceinline__ void qcp_terms(const V3 wc1, const V3 c1, const V3 c2
 // its LDS staging out of the default kernel).
 // PR: reuse effector path prefixes (PathCk) in multi-effector segments solved from registers.
 // HELP: the parent-side values come from the helper wave's record hrec (kHelpF4 float4 at
-// stride 64), not from this wave.
-template <bool STAB, bool PR, int TA, bool HELP, class LV, class FP, class IP>
-__device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j, int m, size_t s, const LV &L, const FP G, const FP TG,
+// stride 64), not from this wave.  XS: the build serves split-exchange tasks (xs, staging 4 /
+// 5): only the two-waves-per-SIMD build, so that the one-wave kernels keep their registers.
+template <bool STAB, bool PR, int TA, bool HELP, bool XS, class LV, class FP, class IP>
+__device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j, int m, int xs, size_t s, const LV &L, const FP G, const FP TG,
 		const FP ST, const IP SF, const FP HS, const FP OE, const FP MS, double &prev_dev, const EffPre &pre, bool hoist, bool dbh,
 		const float4 *hrec, int *hflB, int hseq, bool *hstuck MBIK_PROF_PARAM) {
 	MBIK_PROF_T(pt0);
@@ -1044,6 +1063,83 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 			translation = tc - mc;
 		}
 		qrot = qcp_single(mvd, tgt);
+	} else if (XS && xs) {
+		// Split-exchange (staging 4 / 5; m >= 2, several effectors): lane j of the group builds
+		// the headings of effectors e0+j, e0+j+m, ... with path sharing along its own sequence
+		// (the depth it shares with its previous / next effector is the least shared depth of
+		// the adjacent effectors in between: a lower bound on the true one, since shared path
+		// depths form an ultrametric, so the reused product is a prefix of both paths).  Each
+		// round the group's m effectors' headings go lane to lane (ds_bpermute), and every lane
+		// consumes all of them in the reference's effector order, exactly as the one-lane
+		// branch below does, so every sum rounds the same.  No staging memory.
+		const int lb = (int)__lane_id() - j;
+		auto each = [&](auto &&use) __attribute__((always_inline)) {
+			PathCk pc;
+			pc.d = -1;
+			for (int i0 = e0; i0 < e1; i0 += m) {
+				const int i = i0 + j;
+				Headings Hm;
+				if (i < e1) {
+					int lc[2] = {0, 0};
+					if (i - m >= e0) {
+						lc[0] = t.seg_eff_lcp[i];
+						for (int u = i - m + 1; u < i; u++) lc[0] = min(lc[0], t.seg_eff_lcp[u]);
+					}
+					if (i + m < e1) {
+						lc[1] = t.seg_eff_lcp[i + 1];
+						for (int u = i + 2; u <= i + m; u++) lc[1] = min(lc[1], t.seg_eff_lcp[u]);
+					}
+					effector_headings<TA>(t, t.seg_effs[i], d0, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], Hm, OE, oe_mode,
+							dbh ? &pre.Db : nullptr, PR ? &pc : nullptr, lc);
+				}
+				for (int v = 0; v < m && i0 + v < e1; v++) {
+					Headings H; // (weights and mask only)
+					heading_weights(t, t.seg_effs[i0 + v], hw + t.seg_eff_hoff[i0 + v], H);
+					const int src = lb + v;
+#pragma unroll
+					for (int h = 0; h < 7; h++) {
+						if (H.mask & (1 << h)) {
+							const V3 ht = v3(__shfl(Hm.ht[h].x, src), __shfl(Hm.ht[h].y, src), __shfl(Hm.ht[h].z, src));
+							const V3 hm = v3(__shfl(Hm.hm[h].x, src), __shfl(Hm.hm[h].y, src), __shfl(Hm.hm[h].z, src));
+							use(ht, hm, H.w[h]);
+						}
+					}
+				}
+			}
+		};
+		V3 mc = v3(0, 0, 0), tc = v3(0, 0, 0);
+		if (translate) {
+			double wsum = 0;
+			each([&](V3 ht, V3 hm, double w) __attribute__((always_inline)) {
+				mc = mc + hm * (float)w;
+				tc = tc + ht * (float)w;
+				wsum += w;
+			});
+			if (wsum > 0) {
+				mc = divs(mc, (float)wsum);
+				tc = divs(tc, (float)wsum);
+			}
+			translation = tc - mc;
+		}
+		QSums S = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+		const V3 nmc = mc * -1.0f, ntc = tc * -1.0f;
+		each([&](V3 ht, V3 hm, double w) __attribute__((always_inline)) {
+			V3 c1 = translate ? ht + ntc : ht;
+			V3 c2 = translate ? hm + nmc : hm;
+			V3 wc1 = c1 * (float)w;
+			S.ss1 += (double)dot(wc1, c1);
+			S.ss2 += w * (double)dot(c2, c2);
+			S.xx += (double)(wc1.x * c2.x);
+			S.xy += (double)(wc1.x * c2.y);
+			S.xz += (double)(wc1.x * c2.z);
+			S.yx += (double)(wc1.y * c2.x);
+			S.yy += (double)(wc1.y * c2.y);
+			S.yz += (double)(wc1.y * c2.z);
+			S.zx += (double)(wc1.z * c2.x);
+			S.zy += (double)(wc1.z * c2.y);
+			S.zz += (double)(wc1.z * c2.z);
+		});
+		qrot = qcp_adjugate(S);
 	} else if (m == 1 || nh == 0) {
 		// Several headings (or none: a pinless root segment, whose sums stay zero), one lane or
 		// every lane of the group alike; only nh >= 2 segments own a staged-heading LDS area
@@ -1543,7 +1639,7 @@ __device__ __forceinline__ int row_steps(const DevPlan &t, int r, int seg_lo, in
 	return __builtin_amdgcn_readfirstlane(n);
 }
 
-template <bool STAB, int PL, bool HOIST = true, bool T32 = true, bool HELP = false>
+template <bool STAB, int PL, bool HOIST = true, bool T32 = true, bool HELP = false, bool XS = false>
 __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int count, const float *__restrict__ pose_in,
 		const float *__restrict__ targets, float *__restrict__ pose_out, int iterations, int seg_lo, int seg_hi) {
 	static_assert(!HELP || (!STAB && PL == 0), "the helper wave serves placement-0 launches without stabilization");
@@ -1705,7 +1801,7 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 					if (r == 0 && q == 0) MBIK_PROF_ADD(20, hw0, hw1);
 #endif
 					if (k0 + q < k1)
-						bone_step<false, kPathReuse, kTab32, true>(t, seg, k0 + q, task.y, task.z, s, L, G, TG, ST, SF, HS, OE, MS, prev_dev,
+						bone_step<false, kPathReuse, kTab32, true, false>(t, seg, k0 + q, task.y, task.z, task.w, s, L, G, TG, ST, SF, HS, OE, MS, prev_dev,
 								pre, hoist, false, ring + slot * (kHelpF4 * 64), b_ready ? nullptr : hfl + 1, seq, &stuck MBIK_PROF_ARG);
 					help_post(hfl + 2, seq + 1);
 					slot = slot + 1 == kHelpSlots ? 0 : slot + 1;
@@ -1741,7 +1837,7 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 				const bool dbh = kDbh && !HOIST && !STAB && t.seg_eff_off[seg + 1] - e0 == 1;
 				if (dbh) pre.Db = ld_soa_basis<TA>(t, t.D, t.eff_bone[t.seg_effs[e0]], 9, 0, s);
 				for (int k = t.seg_bone_off[seg]; k < t.seg_bone_off[seg + 1]; k++)
-					bone_step<STAB, kPathReuse && (HOIST || (PL == 2 && !kNoPrPl2) || kPathReuse2W), TA, false>(t, seg, k, task.y, task.z, s, L, G, TG, ST, SF, HS, OE, MS, prev_dev, pre, hoist, dbh,
+					bone_step<STAB, kPathReuse && (HOIST || (PL == 2 && !kNoPrPl2) || kPathReuse2W), TA, false, XS>(t, seg, k, task.y, task.z, task.w, s, L, G, TG, ST, SF, HS, OE, MS, prev_dev, pre, hoist, dbh,
 							nullptr, nullptr, 0, nullptr MBIK_PROF_ARG);
 			}
 			__syncthreads();
@@ -1787,15 +1883,17 @@ __device__ __forceinline__ int xcd_block() {
 // file, no spills.  2: at most 256 registers, some spilled to scratch, but two one-wave
 // blocks share a SIMD -- for launches whose skeletons no longer fit the chip at once and
 // whose state is not in LDS (mbik_plan_set_waves_per_simd; autotune decides).
-template <bool STAB, int PL, int WPE = MBIK_WAVES_PER_EU, bool T32 = true>
+// XS: the build with split-exchange segments (staging 4 / 5; two waves per SIMD only), a separate
+// instantiation so the other builds keep their register allocation.
+template <bool STAB, int PL, int WPE = MBIK_WAVES_PER_EU, bool T32 = true, bool XS = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void mbik_solve_kernel(DevPlan t, int first, int count, const float *__restrict__ pose_in,
 		const float *__restrict__ targets, float *__restrict__ pose_out, int iterations, int seg_lo, int seg_hi) {
-	solve_block<STAB, PL, WPE == 1, T32>(t, xcd_block(), first, count, pose_in, targets, pose_out, iterations, seg_lo, seg_hi);
+	solve_block<STAB, PL, WPE == 1, T32, false, XS>(t, xcd_block(), first, count, pose_in, targets, pose_out, iterations, seg_lo, seg_hi);
 }
 
 // The same with a helper wave (two waves per block, on two SIMDs of a CU): placement 0, no
 // stabilization, 32-bit table addressing (mbik_plan_set_helper_wave; autotune decides).
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(1, 1))) void mbik_solve_help_kernel(DevPlan t, int first, int count,
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(1, 1))) void mbik_solve_kernel_help(DevPlan t, int first, int count,
 		const float *__restrict__ pose_in, const float *__restrict__ targets, float *__restrict__ pose_out, int iterations, int seg_lo,
 		int seg_hi) {
 	solve_block<false, 0, true, true, true>(t, xcd_block(), first, count, pose_in, targets, pose_out, iterations, seg_lo, seg_hi);
@@ -1996,7 +2094,7 @@ int upload_topology(mbik_plan *p) {
 		if (bytes) std::memcpy(blob.data() + off, data, bytes);
 	};
 	std::vector<int4> rows(h.sched.size());
-	for (size_t i = 0; i < rows.size(); i++) rows[i] = make_int4(h.sched[i].seg, h.sched[i].j, h.sched[i].m, 0);
+	for (size_t i = 0; i < rows.size(); i++) rows[i] = make_int4(h.sched[i].seg, h.sched[i].j, h.sched[i].m, h.sched[i].xs);
 	add(rows.data(), rows.size() * sizeof(int4), 4, d.o_sched);
 #define MBIK_ADD(T, name) \
 	if (std::string(#name) != "sched") add(h.name.data(), h.name.size() * sizeof(h.name[0]), sizeof(T) >= 16 ? 4 : (sizeof(T) >= 8 ? 2 : 1), d.o_##name);
@@ -2034,6 +2132,8 @@ SolveKernel solve_kernel_for(const mbik_plan *p) {
 	static const SolveKernel ks[2][3] = {{mbik_solve_kernel<false, 0>, mbik_solve_kernel<false, 1>, mbik_solve_kernel<false, 2>},
 			{mbik_solve_kernel<true, 0>, mbik_solve_kernel<true, 1>, mbik_solve_kernel<true, 2>}};
 	static const SolveKernel k2[3] = {mbik_solve_kernel<false, 0, 2>, mbik_solve_kernel<false, 1, 2>, mbik_solve_kernel<false, 2, 2>};
+	static const SolveKernel k2x[3] = {mbik_solve_kernel<false, 0, 2, true, true>, mbik_solve_kernel<false, 1, 2, true, true>,
+			mbik_solve_kernel<false, 2, 2, true, true>};
 	// placement 0 with tables of 4 GiB or more: 64-bit element indices
 	static const SolveKernel k64[3] = {mbik_solve_kernel<false, 0, 1, false>, mbik_solve_kernel<true, 0, 1, false>,
 			mbik_solve_kernel<false, 0, 2, false>};
@@ -2042,17 +2142,18 @@ SolveKernel solve_kernel_for(const mbik_plan *p) {
 		for (auto &row : ks)
 			for (SolveKernel k : row) (void)hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 		for (SolveKernel k : k2) (void)hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+		for (SolveKernel k : k2x) (void)hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 		for (SolveKernel k : k64) (void)hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 	});
 	const int pl = std::min(2, std::max(0, (int)h.state_hbm));
 	const bool two = h.waves_per_simd == 2 && h.stabilization_passes == 0;
 	if (pl == 0 && !tables_fit_32(p)) return two ? k64[2] : k64[h.stabilization_passes > 0 ? 1 : 0];
-	if (two) return k2[pl];
+	if (two) return h.has_xs ? k2x[pl] : k2[pl];
 	return ks[h.stabilization_passes > 0 ? 1 : 0][pl];
 }
 
 // Whether a launch of the plan's current layout runs with the helper wave
-// (mbik_solve_help_kernel): asked for, and a layout it serves -- state in LDS, no
+// (mbik_solve_kernel_help): asked for, and a layout it serves -- state in LDS, no
 // stabilization, one wave per SIMD, 32-bit tables -- whose block LDS still fits with the ring.
 bool helper_on(const mbik_plan *p) {
 	const mbik::HostPlan &h = p->host;
@@ -2095,6 +2196,9 @@ int ensure_schedule(mbik_plan *p, int64_t nlaunch) {
 		p->dev.Lg = p->d_locals;
 		p->dev.lg_bytes = (uint32_t)std::min<size_t>(bytes, 0xFFFFFFFFu); // (placement 2 refuses > kMaxBufBytes)
 	}
+	// split-exchange (staging 4 / 5) runs in the 32-bit-table two-wave builds; the 64-bit-index
+	// two-wave build solves those segments alone (4 -> 0) or staged (5 -> 2)
+	if (h.waves_per_simd == 2 && !tables_fit_32(p) && h.staging >= 4) h.staging = h.staging == 4 ? 0 : 2;
 	mbik::build_schedule(h, lanes, nlaunch, p->spw_override, p->interval_override, blocks_per_cu, p, p->cu_count);
 	if (lanes == 0 && h.constraint_mode && h.K > kCmodeLanes)
 		mbik::build_schedule(h, kCmodeLanes, nlaunch, p->spw_override, p->interval_override, blocks_per_cu, p, p->cu_count);
@@ -2364,9 +2468,9 @@ int launch(mbik_plan *p, int first, int count, const float *pose_in, const float
 	if (helper_on(p)) {
 		static std::once_flag honce;
 		std::call_once(honce, [] {
-			(void)hipFuncSetAttribute((const void *)mbik_solve_help_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+			(void)hipFuncSetAttribute((const void *)mbik_solve_kernel_help, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 		});
-		kern = mbik_solve_help_kernel;
+		kern = mbik_solve_kernel_help;
 		lds += kHelpRingBytes;
 		threads = 128;
 	}
@@ -3078,7 +3182,7 @@ int32_t mbik_plan_set_locals_placement(mbik_plan *p, int32_t placement) {
 
 int32_t mbik_plan_set_heading_staging(mbik_plan *p, int32_t staging) {
 	if (!p) return fail(MBIK_EINVAL, "null plan");
-	if (staging < -1 || staging > 3) return fail(MBIK_EINVAL, "staging must be -1 (automatic), 0, 1, 2 or 3");
+	if (staging < -1 || staging > 5) return fail(MBIK_EINVAL, "staging must be -1 (automatic), 0, 1, 2, 3, 4 or 5");
 	p->staging_override = staging;
 	p->sched_K = -1;
 	return MBIK_OK;
@@ -3312,18 +3416,28 @@ int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const flo
 			// a second wave per SIMD only pays where LDS no longer bounds the blocks per CU
 			if (wv == 2 && lh == 0 && locals0 < 0) continue;
 			p->host.state_hbm = lh;
-			for (int stg : {1, 3, 2, 0}) {
+			bool nothing_staged = false;
+			for (int stg : {1, 3, 2, 0, 4, 5}) {
 				if (staging0 >= 0 && stg != staging0) continue;
+				if (stg <= 3 && nothing_staged) continue;   // (the same layouts as the first)
 				if (stg == 2 && !has_staged_root) continue; // (the same layouts as 0)
 				if (stg == 3 && !has_multi_eff) continue;   // (the same layouts as 0)
+				if (stg == 4 && !has_multi_eff) continue;   // (the same layouts as 0)
+				if (stg == 5 && !(has_multi_eff && has_staged_root)) continue; // (as 4, or as 0)
 				p->host.staging = stg;
 				// with the whole state in device memory the interval does not change residency, only
 				// the checkpoint writes against the rebuild products (C5: 2 is 0.7 % faster than 1)
 				const std::vector<int> intervals = lh == 2 ? std::vector<int>{1, 2} : std::vector<int>{1, 2, 4, 1 << 20};
 				for (int c : intervals) {
 					int last_blocks = -1;
-					for (int spw = 64; spw >= 1; spw--) {
+					bool split = true;
+					for (int spw = 64; spw >= 1 && split; spw--) {
 						mbik::build_schedule(p->host, ln, count, spw, c, blocks_per_cu, p, p->cu_count);
+						// 4 / 5 with no segment split over lanes (one lane per skeleton) are 0 / 2
+						if (stg >= 4 && !p->host.has_xs) {
+							split = false;
+							break;
+						}
 						if (p->host.spw != spw) continue; // capped by 64 / K or by LDS
 						const int blocks = blocks_per_cu(p, p->host.lds_block_bytes);
 						if (blocks != last_blocks) {
@@ -3332,7 +3446,7 @@ int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const flo
 						}
 					}
 				}
-				if (p->host.hs_floats == 0) break; // nothing is staged: the no-staging layouts are the same
+				if (stg <= 3 && p->host.hs_floats == 0) nothing_staged = true; // nothing is staged: 3, 2, 0 are the same
 			}
 		}
 	}
@@ -3735,10 +3849,10 @@ int32_t mbik_group_solve(mbik_group *g, const int32_t *first, const int32_t *cou
 		if (!pose_in[i] || !pose_out[i] || (p->host.P > 0 && !targets[i])) return fail(MBIK_EINVAL, "null buffer");
 		int rc = p->host.P > 0 ? ensure_schedule(p, c) : MBIK_OK;
 		if (rc) return rc;
-		if (p->host.constraint_mode || p->host.P == 0 || p->host.state_hbm != 0 || !tables_fit_32(p)) {
+		if (p->host.constraint_mode || p->host.P == 0 || p->host.state_hbm != 0 || !tables_fit_32(p) || p->host.has_xs) {
 			// constraint_mode plans have their own kernel, so do plans laid out with their
-			// locals in HBM and plans whose setup tables need 64-bit indices; pinless plans
-			// only copy
+			// locals in HBM, plans whose setup tables need 64-bit indices and plans with
+			// split-exchange segments (the two-wave build); pinless plans only copy
 			rc = launch(p, f, c, pose_in[i], targets[i], pose_out[i], stream, p->host.iterations, 0, p->host.NS - 1);
 			if (rc) return rc;
 			continue;

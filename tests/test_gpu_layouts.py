@@ -116,8 +116,56 @@ def test_unstaged_headings_bitwise_vs_oracle(oracle, mbik, cfg, n, stab, lanes, 
 def test_staging_argument_check(mbik):
     plan = Plan.from_workload(W.generate(3, 2))
     with pytest.raises(_lib.MbikError):
-        plan.set_heading_staging(4)
+        plan.set_heading_staging(6)
     plan.set_heading_staging(-1)
+
+
+@pytest.mark.parametrize("cfg,n", [(2, 48), (3, 48), (4, 16), (5, 6)])
+@pytest.mark.parametrize("staging", [4, 5])
+@pytest.mark.parametrize("placement", [0, 1, 2])
+@pytest.mark.parametrize("lanes", [0, 16])
+def test_split_exchange_bitwise_vs_oracle(oracle, mbik, cfg, n, staging, placement, lanes):
+    """mbik_plan_set_heading_staging(4 | 5) in the two-wave build: a multi-effector segment's
+    lanes build alternate effectors' headings and read each other's lane to lane, every lane
+    summing all of them in order (5: translating roots staged in memory instead); bitwise."""
+    wl = W.generate(cfg, n, first=31000)
+    ref = oracle.Oracle(wl).solve(wl.pose, wl.targets, threads=8)
+    plan = Plan.from_workload(wl)
+    plan.set_layout(lanes, 0, 0)
+    plan.set_waves_per_simd(2)
+    plan.set_locals_placement(placement)
+    plan.set_heading_staging(staging)
+    got = plan.solve_host(wl.pose, wl.targets)
+    assert plan.info()["heading_staging"] == staging
+    assert_parity(got, ref, f"C{cfg} staging={staging} placement={placement} lanes={lanes}")
+
+
+@pytest.mark.parametrize("cfg,n", [(4, 16), (5, 6)])
+def test_split_exchange_in_one_wave_build_solves_alone(oracle, mbik, cfg, n):
+    """The one-wave build has no split-exchange code: staging 4 / 5 there solve those segments
+    alone (as 0 / 2) and stay exact; a group with a split-exchange plan launches it on its own."""
+    from many_bone_ik_amd.solver import Group
+    import torch
+    wl = W.generate(cfg, n, first=32000)
+    ref = oracle.Oracle(wl).solve(wl.pose, wl.targets, threads=8)
+    plan = Plan.from_workload(wl)
+    plan.set_heading_staging(4)
+    assert_parity(plan.solve_host(wl.pose, wl.targets), ref, f"C{cfg} staging 4, one wave")
+    plan.set_waves_per_simd(2)
+    dev = torch.device("cuda", 0)
+    pi = torch.from_numpy(wl.pose).to(dev)
+    tg = torch.from_numpy(wl.targets).to(dev)
+    po = torch.empty_like(pi)
+    wl3 = W.generate(3, 24, first=50)
+    plan3 = Plan.from_workload(wl3)
+    pi3 = torch.from_numpy(wl3.pose).to(dev)
+    tg3 = torch.from_numpy(wl3.targets).to(dev)
+    po3 = torch.empty_like(pi3)
+    grp = Group([plan, plan3])
+    grp.solve([pi.data_ptr(), pi3.data_ptr()], [tg.data_ptr(), tg3.data_ptr()], [po.data_ptr(), po3.data_ptr()])
+    torch.cuda.synchronize()
+    assert_parity(po.cpu().numpy(), ref, f"group: C{cfg} split-exchange plan")
+    assert_parity(po3.cpu().numpy(), oracle.Oracle(wl3).solve(wl3.pose, wl3.targets, threads=8), "group: LDS plan")
 
 
 @pytest.mark.parametrize("cfg,n", [(1, 8), (2, 48), (3, 48), (4, 16), (5, 6)])
