@@ -617,7 +617,51 @@ void build_schedule(HostPlan &p, int32_t lanes, int64_t nlaunch, int32_t spw_ove
 	p.sched.clear();
 	p.nrows = 0;
 	p.has_xs = false;
+	p.has_chain = false;
+	// A level with more segments than lanes runs in several rows of single-lane tasks.  Its
+	// segments are independent, so the rows are packed instead: each lane gets a sequence of
+	// segments (longest processing time first, by an estimate of each segment's step work:
+	// per bone-step its effectors' path walks plus a constant), and the kernel runs a lane's
+	// sequence back to back with no barrier between the rows (SCHED_CHAIN).  A lane then waits
+	// for the most loaded lane of the level, not for the longest segment of every row.
+	std::vector<int> depth(p.B, 0);
+	for (size_t e = 0; e + 1 < p.eff_path_off.size(); e++)
+		for (int i = p.eff_path_off[e]; i < p.eff_path_off[e + 1]; i++) depth[p.eff_path[i]] = i - p.eff_path_off[e];
+	auto seg_cost = [&](int sg) {
+		int64_t c = 0;
+		for (int k = p.seg_bone_off[sg]; k < p.seg_bone_off[sg + 1]; k++) {
+			c += 24;
+			for (int i = p.seg_eff_off[sg]; i < p.seg_eff_off[sg + 1]; i++) {
+				const int e = p.seg_effs[i];
+				c += std::max(0, p.eff_path_off[e + 1] - p.eff_path_off[e] - 1 - depth[p.seg_bones[k]]);
+			}
+		}
+		return c;
+	};
 	for (auto &l : lev) {
+		if ((int)l.size() > K && !p.constraint_mode) {
+			std::vector<int> order(l);
+			std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return seg_cost(a) > seg_cost(b); });
+			std::vector<std::vector<int>> per(K);
+			std::vector<int64_t> load(K, 0);
+			for (int sg : order) {
+				const int i = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+				per[i].push_back(sg);
+				load[i] += seg_cost(sg);
+			}
+			size_t nr = 0;
+			for (auto &v : per) nr = std::max(nr, v.size());
+			for (size_t q = 0; q < nr; q++) {
+				const int32_t ch = q > 0 ? SCHED_CHAIN : 0;
+				std::vector<SchedTask> row(K, SchedTask{-1, 0, 1, ch});
+				for (int i = 0; i < K; i++)
+					if (q < per[i].size()) row[i] = SchedTask{per[i][q], 0, 1, ch};
+				p.sched.insert(p.sched.end(), row.begin(), row.end());
+				p.nrows++;
+			}
+			p.has_chain |= nr > 1;
+			continue;
+		}
 		for (size_t start = 0; start < l.size(); start += K) {
 			int cnt = (int)std::min<size_t>(K, l.size() - start);
 			int m = K >> ceil_log2(cnt);
@@ -635,7 +679,7 @@ void build_schedule(HostPlan &p, int32_t lanes, int64_t nlaunch, int32_t spw_ove
 				// (the two-waves-per-SIMD build is the one that serves them; one wave: solo)
 				const bool xs = solo && multi && m >= 2 && (p.staging == 4 || p.staging == 5) && p.waves_per_simd == 2;
 				for (int j = 0; j < m; j++)
-					row[i * m + j] = xs ? SchedTask{sg, j, m, 1} : (solo ? SchedTask{sg, 0, 1, 0} : SchedTask{sg, j, m, 0});
+					row[i * m + j] = xs ? SchedTask{sg, j, m, SCHED_XS} : (solo ? SchedTask{sg, 0, 1, 0} : SchedTask{sg, j, m, 0});
 				p.has_xs |= xs;
 			}
 			p.sched.insert(p.sched.end(), row.begin(), row.end());

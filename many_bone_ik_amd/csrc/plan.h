@@ -58,9 +58,11 @@ struct SchedTask {
 	int32_t seg;  // -1 idle
 	int32_t j;    // index of this lane inside the segment's lane group
 	int32_t m;    // lanes in the group (power of two, aligned)
-	int32_t xs;   // 1: split-exchange (staging 4/5): the group's lanes build alternate effectors' headings and
-	              // share them through cross-lane reads; every lane sums them all in order (no staging memory)
+	int32_t xs;   // bit 0 (SCHED_XS): split-exchange (staging 4/5): the group's lanes build alternate effectors'
+	              // headings and share them through cross-lane reads; every lane sums them all in order (no
+	              // staging memory).  bit 1 (SCHED_CHAIN): this row continues the previous one's packed level
 };
+constexpr int32_t SCHED_XS = 1, SCHED_CHAIN = 2;
 
 struct HostPlan {
 	// ---- topology (shared by the batch) ----
@@ -112,7 +114,8 @@ struct HostPlan {
 	// the other multi-effector segments as in 4.  Not for constraint_mode (its lanes own tree
 	// ranges).
 	int staging = 1;
-	bool has_xs = false; // the schedule has split-exchange tasks (staging 4 / 5, two-wave build only)
+	bool has_xs = false;     // the schedule has split-exchange tasks (staging 4 / 5, two-wave build only)
+	bool has_chain = false;  // the schedule has packed levels (rows chained without a barrier)
 	// Where the per-skeleton solve state lives during a launch: 0 all of it in LDS; 1 the
 	// bone local transforms L in a per-skeleton device-memory area (L2-resident), the rest in
 	// LDS; 2 all of it in device memory (LDS holds only the block's topology copy).  Less LDS

@@ -1801,7 +1801,7 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 					if (r == 0 && q == 0) MBIK_PROF_ADD(20, hw0, hw1);
 #endif
 					if (k0 + q < k1)
-						bone_step<false, kPathReuse, kTab32, true, false>(t, seg, k0 + q, task.y, task.z, task.w, s, L, G, TG, ST, SF, HS, OE, MS, prev_dev,
+						bone_step<false, kPathReuse, kTab32, true, false>(t, seg, k0 + q, task.y, task.z, task.w & mbik::SCHED_XS, s, L, G, TG, ST, SF, HS, OE, MS, prev_dev,
 								pre, hoist, false, ring + slot * (kHelpF4 * 64), b_ready ? nullptr : hfl + 1, seq, &stuck MBIK_PROF_ARG);
 					help_post(hfl + 2, seq + 1);
 					slot = slot + 1 == kHelpSlots ? 0 : slot + 1;
@@ -1820,27 +1820,44 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 		}
 		MBIK_PROF_T(pg1);
 		MBIK_PROF_ADD(5, pg0, pg1);
-		for (int r = 0; r < t.nrows; r++) {
-			const int4 task = t.sched[r * K + role];
-			if (valid && task.x >= seg_lo && task.x <= seg_hi) {
-				double prev_dev = INFINITY; // reset after the segment root bone (:178-180)
-				// A single-effector segment solved by one lane (or with a single heading) reads
-				// the same effector data at every bone-step: load it once for the segment.
-				const int seg = task.x, e0 = t.seg_eff_off[seg];
-				EffPre pre;
-				// (not in the two-waves-per-SIMD build: the hoisted data's ~66 registers are what
-				// push that build past 256 and into scratch spills)
-				const bool hoist = HOIST && kEffHoist && !STAB && t.seg_eff_off[seg + 1] - e0 == 1 && (task.z == 1 || t.seg_nh[seg] == 1);
-				if (hoist) load_eff<TA>(t, t.seg_effs[e0], TG, s, t.seg_hw + t.seg_hw_off[seg] + t.seg_eff_hoff[e0], pre);
-				// (kDbh: the two-wave build may hoist only the effector's bone-direction basis;
-				// off by default since round 2, see kDbh)
-				const bool dbh = kDbh && !HOIST && !STAB && t.seg_eff_off[seg + 1] - e0 == 1;
-				if (dbh) pre.Db = ld_soa_basis<TA>(t, t.D, t.eff_bone[t.seg_effs[e0]], 9, 0, s);
-				for (int k = t.seg_bone_off[seg]; k < t.seg_bone_off[seg + 1]; k++)
-					bone_step<STAB, kPathReuse && (HOIST || (PL == 2 && !kNoPrPl2) || kPathReuse2W), TA, false, XS>(t, seg, k, task.y, task.z, task.w, s, L, G, TG, ST, SF, HS, OE, MS, prev_dev, pre, hoist, dbh,
-							nullptr, nullptr, 0, nullptr MBIK_PROF_ARG);
+		for (int r = 0; r < t.nrows;) {
+			// rows r .. r1-1: one row, or a packed level (SCHED_CHAIN rows, build_schedule) whose
+			// lanes each run their sequence of segments back to back, without a barrier
+			int r1 = r + 1;
+			while (r1 < t.nrows && (t.sched[r1 * K].w & mbik::SCHED_CHAIN)) r1++;
+			int rr = r - 1, k = 0, ke = 0, seg = 0;
+			int4 task = make_int4(-1, 0, 1, 0);
+			double prev_dev = INFINITY;
+			EffPre pre;
+			bool hoist = false, dbh = false;
+			for (;;) {
+				while (k >= ke && rr + 1 < r1) {
+					task = t.sched[++rr * K + role];
+					if (valid && task.x >= seg_lo && task.x <= seg_hi) {
+						seg = task.x;
+						k = t.seg_bone_off[seg];
+						ke = t.seg_bone_off[seg + 1];
+						prev_dev = INFINITY; // reset after the segment root bone (:178-180)
+						// A single-effector segment solved by one lane (or with a single heading)
+						// reads the same effector data at every bone-step: load it once for the segment.
+						// (not in the two-waves-per-SIMD build: the hoisted data's ~66 registers are
+						// what push that build past 256 and into scratch spills)
+						const int e0 = t.seg_eff_off[seg];
+						hoist = HOIST && kEffHoist && !STAB && t.seg_eff_off[seg + 1] - e0 == 1 && (task.z == 1 || t.seg_nh[seg] == 1);
+						if (hoist) load_eff<TA>(t, t.seg_effs[e0], TG, s, t.seg_hw + t.seg_hw_off[seg] + t.seg_eff_hoff[e0], pre);
+						// (kDbh: the two-wave build may hoist only the effector's bone-direction basis;
+						// off by default since round 2, see kDbh)
+						dbh = kDbh && !HOIST && !STAB && t.seg_eff_off[seg + 1] - e0 == 1;
+						if (dbh) pre.Db = ld_soa_basis<TA>(t, t.D, t.eff_bone[t.seg_effs[e0]], 9, 0, s);
+					}
+				}
+				if (k >= ke) break;
+				bone_step<STAB, kPathReuse && (HOIST || (PL == 2 && !kNoPrPl2) || kPathReuse2W), TA, false, XS>(t, seg, k, task.y, task.z,
+						task.w & mbik::SCHED_XS, s, L, G, TG, ST, SF, HS, OE, MS, prev_dev, pre, hoist, dbh, nullptr, nullptr, 0, nullptr MBIK_PROF_ARG);
+				k++;
 			}
 			__syncthreads();
+			r = r1;
 		}
 	}
 	MBIK_PROF_T(pk2);
@@ -2158,6 +2175,7 @@ SolveKernel solve_kernel_for(const mbik_plan *p) {
 bool helper_on(const mbik_plan *p) {
 	const mbik::HostPlan &h = p->host;
 	if (p->helper_override != 1) return false;
+	// (packed levels run row by row there: both waves walk the same rows)
 	if (h.state_hbm != 0 || h.stabilization_passes != 0 || h.waves_per_simd != 1 || h.constraint_mode || !tables_fit_32(p)) return false;
 	const size_t lds = ((size_t)h.spw * p->dev.lds_stride + p->dev.topo_words) * sizeof(float) + kHelpRingBytes;
 	return lds <= 160 * 1024;

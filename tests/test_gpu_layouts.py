@@ -363,3 +363,22 @@ def test_state_in_hbm_reads_rebuilt_setup_tables(oracle, mbik, waves):
     want = fresh.solve_host(wl.pose, wl.targets)
     assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
     assert not np.array_equal(got.view(np.uint32), first.view(np.uint32))
+
+
+@pytest.mark.parametrize("cfg,n,lanes", [(5, 12, 8), (5, 12, 4), (4, 16, 4), (2, 24, 2)])
+@pytest.mark.parametrize("stab", [0, 2])
+@pytest.mark.parametrize("placement,waves", [(0, 1), (1, 2), (2, 2)])
+def test_packed_levels_bitwise_vs_oracle(oracle, mbik, cfg, n, lanes, stab, placement, waves):
+    """A sibling level wider than the lane count is packed (build_schedule, SCHED_CHAIN): each
+    lane runs its own sequence of segments back to back, balanced by estimated step work (C5's
+    16 fingers of 6-14 bones on 8 or 4 lanes); sibling segments are independent, so the results
+    stay bitwise equal."""
+    wl = W.generate(cfg, n, first=33000)
+    ref = oracle.Oracle(wl, stabilization_passes=stab).solve(wl.pose, wl.targets, threads=8)
+    plan = Plan.from_workload(wl, stabilization_passes=stab)
+    plan.set_layout(lanes, 0, 0)
+    plan.set_locals_placement(placement)
+    plan.set_waves_per_simd(waves)
+    got = plan.solve_host(wl.pose, wl.targets)
+    assert plan.info()["lanes_per_skeleton"] == lanes
+    assert_parity(got, ref, f"C{cfg} packed levels lanes={lanes} stab={stab} placement={placement} waves={waves}")

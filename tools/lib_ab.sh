@@ -1,0 +1,17 @@
+#!/bin/bash
+# Same-box A/B of the in-tree library against build/abl/libmbik_abl_<tag>.so on pinned layouts,
+# interleaved twice:   tools/lib_ab.sh <tag> <config>:<layout> [...]
+TAG=$1; shift
+mkdir -p gpurun_out
+for rep in 1 2; do
+for CL in "$@"; do
+  CFG=${CL%%:*}; L=${CL#*:}
+  for lib in new $TAG; do
+    if [ $lib = new ]; then unset MBIK_LIB_OVERRIDE; else export MBIK_LIB_OVERRIDE=$PWD/build/abl/libmbik_abl_$lib.so; fi
+    out=gpurun_out/libab_${lib}_c${CFG}_${L//:/_}_r$rep.json
+    timeout -k 10 150 python bench.py --config $CFG --layout $L --steps 20 --warmup 3 --no-cpu-baseline > $out 2>/dev/null || exit 1
+    python3 -c "import json;d=json.loads(open('$out').read().strip().splitlines()[-1]);print('$lib', 'c$CFG', '$L', 'r$rep', round(d['ms_per_step'],4), d['parity'].get('bitwise_equal'))"
+  done
+done
+done
+unset MBIK_LIB_OVERRIDE
