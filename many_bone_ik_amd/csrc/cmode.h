@@ -363,7 +363,9 @@ __device__ void cmode_step(const CmodeLane<NB32> &C, int seg, int k, const float
 // 1003 vs 56 ms; LDS caps how many skeletons are resident;
 // profiles/r01_cmode_layout_sweep.jsonl).
 constexpr int kCmodeMaxWaves = 4; // waves per constraint_mode block (launch bound)
-template <bool STAB, bool NB32>
+// CHAIN: the schedule has packed levels (SCHED_CHAIN rows); plans without them keep the plain
+// row loop (its registers: the packed loop measured +2 % on C2).
+template <bool STAB, bool NB32, bool CHAIN = false>
 __global__ __launch_bounds__(64 * kCmodeMaxWaves) void mbik_cmode_kernel(DevPlan t, CmodeState c, int first, int count,
 		const float *__restrict__ pose_in, const float *__restrict__ targets, float *__restrict__ pose_out, int iterations,
 		int seg_lo, int seg_hi) {
@@ -425,6 +427,7 @@ __global__ __launch_bounds__(64 * kCmodeMaxWaves) void mbik_cmode_kernel(DevPlan
 	__syncthreads();
 	const float *tg = targets + (size_t)local * P * 12;
 	for (int it = 0; it < iterations; it++) {
+		if constexpr (!CHAIN) {
 		for (int r = 0; r < t.nrows; r++) {
 			const int4 task = t.sched[r * K + role];
 			if (valid && task.x >= seg_lo && task.x <= seg_hi && task.y == 0) {
@@ -454,6 +457,70 @@ __global__ __launch_bounds__(64 * kCmodeMaxWaves) void mbik_cmode_kernel(DevPlan
 			MBIK_PROF_T(r1);
 			MBIK_PROF_ADD(8, r0, r1);
 			__syncthreads();
+		}
+		} else {
+		for (int r = 0; r < t.nrows;) {
+			// rows r .. r1-1: one row, or a packed level (SCHED_CHAIN rows, at most four
+			// segments per lane): each lane runs its segments back to back.  Nothing above the
+			// level changes during it, so a sibling's private reads of the chains above its root
+			// give the same bits before or after another sibling's cleaning; every segment's
+			// pending chain is kept (p0..p3) and cleaned after the level.
+			int r1 = r + 1;
+			while (r1 < t.nrows && (t.sched[r1 * K].w & mbik::SCHED_CHAIN)) r1++;
+			int rr = r - 1, k = 0, ke = 0, seg = 0;
+			int p1 = -1, p2 = -1, p3 = -1;
+			double prev_dev = INFINITY;
+			for (;;) {
+				while (k >= ke && rr + 1 < r1) {
+					const int4 task = t.sched[++rr * K + role];
+					if (valid && task.x >= seg_lo && task.x <= seg_hi && task.y == 0) {
+						if (pend >= 0) {
+							p3 = p2;
+							p2 = p1;
+							p1 = pend;
+							pend = -1;
+						}
+						seg = task.x;
+						const int root = t.seg_bones[t.seg_bone_off[seg + 1] - 1];
+						C.lo = pre[root];
+						C.hi = pre[root] + sub[root];
+						k = t.seg_bone_off[seg];
+						ke = t.seg_bone_off[seg + 1];
+						prev_dev = INFINITY; // reset after the segment root bone (:178-180)
+					}
+				}
+				if (k >= ke) break;
+				cmode_step<STAB, NB32>(C, seg, k, tg, OE, prev_dev);
+				k++;
+			}
+			__syncthreads();
+			// The cleaning the reference's first read above the segment root did: the dirty
+			// chain from the recorded node up, one lane at a time (siblings share it).
+			MBIK_PROF_T(r0);
+#pragma unroll
+			for (int q = 0; q < 4; q++) {
+				uint64_t todo = __ballot(pend >= 0);
+				while (todo) {
+					const int l = __ffsll((unsigned long long)todo) - 1;
+					todo &= todo - 1;
+					if (lane == l) {
+						C.lo = 0;
+						C.hi = 0x7fffffff;
+						(void)C.pose_global(pend);
+					}
+					__threadfence_block();
+				}
+				pend = p1;
+				p1 = p2;
+				p2 = p3;
+				p3 = -1;
+				if (!__any(pend >= 0)) break;
+			}
+			MBIK_PROF_T(r1);
+			MBIK_PROF_ADD(8, r0, r1);
+			__syncthreads();
+			r = r1;
+		}
 		}
 	}
 	bool bad = false;

@@ -639,13 +639,16 @@ void build_schedule(HostPlan &p, int32_t lanes, int64_t nlaunch, int32_t spw_ove
 		return c;
 	};
 	for (auto &l : lev) {
-		if ((int)l.size() > K && !p.constraint_mode) {
+		// (constraint_mode keeps at most four pending chain cleanings per lane: cmode.h)
+		if ((int)l.size() > K && (!p.constraint_mode || (int)l.size() <= 4 * K)) {
 			std::vector<int> order(l);
 			std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return seg_cost(a) > seg_cost(b); });
 			std::vector<std::vector<int>> per(K);
 			std::vector<int64_t> load(K, 0);
 			for (int sg : order) {
-				const int i = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+				int i = -1;
+				for (int q = 0; q < K; q++)
+					if ((!p.constraint_mode || per[q].size() < 4) && (i < 0 || load[q] < load[i])) i = q;
 				per[i].push_back(sg);
 				load[i] += seg_cost(sg);
 			}

@@ -2463,11 +2463,17 @@ int launch(mbik_plan *p, int first, int count, const float *pose_in, const float
 			(void)hipFuncSetAttribute((const void *)mbik_cmode_kernel<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 			(void)hipFuncSetAttribute((const void *)mbik_cmode_kernel<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 			(void)hipFuncSetAttribute((const void *)mbik_cmode_kernel<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+			(void)hipFuncSetAttribute((const void *)mbik_cmode_kernel<false, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+			(void)hipFuncSetAttribute((const void *)mbik_cmode_kernel<true, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+			(void)hipFuncSetAttribute((const void *)mbik_cmode_kernel<false, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+			(void)hipFuncSetAttribute((const void *)mbik_cmode_kernel<true, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 		});
 		// node caches below 4 GiB: buffer-resource addressing (cmode.h, NB32)
 		const bool nb32 = node_area_floats(3 * h.B + 2 * h.NC, (size_t)h.N) * sizeof(float) < (size_t(1) << 32) && tables_fit_32(p);
-		auto ck = h.stabilization_passes > 0 ? (nb32 ? mbik_cmode_kernel<true, true> : mbik_cmode_kernel<true, false>)
-											 : (nb32 ? mbik_cmode_kernel<false, true> : mbik_cmode_kernel<false, false>);
+		auto ck = h.has_chain ? (h.stabilization_passes > 0 ? (nb32 ? mbik_cmode_kernel<true, true, true> : mbik_cmode_kernel<true, false, true>)
+												 : (nb32 ? mbik_cmode_kernel<false, true, true> : mbik_cmode_kernel<false, false, true>))
+							  : (h.stabilization_passes > 0 ? (nb32 ? mbik_cmode_kernel<true, true> : mbik_cmode_kernel<true, false>)
+												 : (nb32 ? mbik_cmode_kernel<false, true> : mbik_cmode_kernel<false, false>));
 		const int per_block = p->cm.spw * p->cm.wpb;
 		hipLaunchKernelGGL(ck, dim3((unsigned)((count + per_block - 1) / per_block)), dim3(64 * p->cm.wpb), clds, stream, p->dev,
 				p->cm, first, count, pose_in, targets, pose_out, iterations, seg_lo, seg_hi);
