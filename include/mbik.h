@@ -190,7 +190,9 @@ int32_t mbik_plan_set_waves_per_simd(mbik_plan *plan, int32_t waves);
  * It pays where SIMDs would otherwise idle: launches resident at once with their state in LDS
  * (a frame of BASELINE configs[1]).  Serves state placement 0 without stabilization; other
  * layouts ignore it.  0 off, -1 (default) automatic: off until mbik_plan_autotune has timed
- * it on a fully resident launch.  Results do not depend on it. */
+ * it on a fully resident launch.  Results do not depend on it.  Every wait between the two
+ * waves has an exit; a wave that took it (an ordering error, never a data-dependent event)
+ * is reported as MBIK_EHIP by the synchronous calls (mbik_plan_autotune, mbik_solve_host). */
 int32_t mbik_plan_set_helper_wave(mbik_plan *plan, int32_t helper);
 /* How the solve addresses the per-skeleton setup tables (D, CF, CD).  0 (default): with
  * 32-bit offsets from a buffer resource when every table is below 4 GiB, else with 64-bit

@@ -2181,6 +2181,18 @@ bool helper_on(const mbik_plan *p) {
 	return lds <= 160 * 1024;
 }
 
+// After a synchronized helper-wave launch: a wave that gave up waiting (help_wait's exit, a
+// protocol error) leaves its count in g_mbik_help_stuck; report it instead of returning
+// results computed from unfinished records.
+int helper_stuck_check() {
+	unsigned int n = 0;
+	if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_mbik_help_stuck), sizeof(n)) != hipSuccess) return fail(MBIK_EHIP, "hipMemcpyFromSymbol");
+	if (n == 0) return MBIK_OK;
+	const unsigned int z = 0;
+	(void)hipMemcpyToSymbol(HIP_SYMBOL(g_mbik_help_stuck), &z, sizeof(z));
+	return fail(MBIK_EHIP, "helper wave: a wave timed out waiting for its partner (" + std::to_string(n) + " waves); results invalid");
+}
+
 // Resident one-wave blocks per CU for a block's LDS size, from the runtime's occupancy
 // query on the kernel instantiation the plan launches (LDS granularity and registers).
 int blocks_per_cu(void *ctx, int64_t lds_bytes) {
@@ -3379,6 +3391,7 @@ static int autotune_helper(mbik_plan *p, int first, int count, const float *pose
 	}
 	(void)hipEventDestroy(e0);
 	(void)hipEventDestroy(e1);
+	if (rc == MBIK_OK) rc = helper_stuck_check();
 	p->helper_override = rc == MBIK_OK && ms[1] * 1.015f < ms[0] ? 1 : 0;
 	return rc;
 }
@@ -3957,9 +3970,10 @@ int32_t mbik_solve_host(mbik_plan *p, int32_t first, int32_t count, const float 
 		return fail(MBIK_EHIP, "hipMemcpy H2D");
 	int rc = launch(p, first, count, p->d_in, p->d_tg, p->d_out, nullptr, h.iterations, 0, h.NS - 1);
 	if (rc) return rc;
+	const bool helped = helper_on(p);
 	if (hipMemcpy(pose_out, p->d_out, need * h.B * 10 * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess)
 		return fail(MBIK_EHIP, std::string("hipMemcpy D2H / kernel: ") + hipGetErrorString(hipGetLastError()));
-	return MBIK_OK;
+	return helped ? helper_stuck_check() : MBIK_OK;
 }
 
 } // extern "C"
