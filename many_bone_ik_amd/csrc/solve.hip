@@ -850,7 +850,8 @@ __device__ __forceinline__ void wave_sync_lds() {
 //   and the twist limit's half cosine (ik_bone_segment_3d.cpp:129-154, ik_kusudama_3d.cpp:117-132).
 // Same operations on the same inputs: the record's values are the bits the solving wave would
 // have computed.  Ring: kHelpSlots records of kHelpF4 float4 per lane, [slot][field][64 lanes];
-// three LDS counters (records produced / consumed, iterations finished) order the two waves.
+// four LDS counters (part A produced, part B produced, records consumed, iterations finished)
+// order the two waves.
 constexpr int kHelpF4 = 18, kHelpSlots = 4;
 constexpr int kHelpRingBytes = kHelpSlots * kHelpF4 * 64 * 16 + 16;
 enum HelpField { HF_P = 0, HF_GB = 12, HF_PINV = 24, HF_PNP = 33, HF_STO = 36, HF_HC = 43, HF_DB = 44, HF_GTC = 53, HF_GTCI = 62 };
