@@ -102,6 +102,9 @@ struct DevPlan {
 	float *Lg = nullptr, *Sg = nullptr;
 	int state_stride = 0;
 	uint32_t lg_bytes = 0, sg_bytes = 0; // their sizes (< 4 GiB: buffer-resource addressing)
+	// state_hbm 2: the checkpoint globals, skeleton-tiled like the locals, [N/kLocTile][n_gck][3][kLocTile][4]
+	float *Gg = nullptr;
+	uint32_t gg_bytes = 0;
 };
 
 // ------------------------------------------------------------------------------------
@@ -303,6 +306,10 @@ struct LocV {
 	}
 };
 using LocContig = LocV<12, 4, float *>;
+// The checkpoint globals G: transform i at p + 12 i (LDS, placements 0 / 1); placement 2 keeps
+// them skeleton-tiled like its locals (LocTiled), so a role's lanes read whole lines.
+template <class PT>
+using GFlat = LocV<12, 4, PT>;
 template <class PT>
 using LocTiled = LocV<12 * kLocTile, 4 * kLocTile, PT>;
 // SoA per-skeleton tables: element (item, field) of skeleton s.
@@ -933,15 +940,15 @@ __device__ __forceinline__ void hw_store(float4 *rec, const float *f, int f4a, i
 	for (int i = f4a; i < f4b; i++) rec[i * 64] = make_float4(f[4 * i], f[4 * i + 1], f[4 * i + 2], f[4 * i + 3]);
 }
 // part A: P and Gb (float4 fields 0-5)
-template <class LV, class FP>
-__device__ __forceinline__ void help_part_a(const DevPlan &t, int k, const LV &L, const FP G, float4 *rec, X3 &P, B3 &Gbb) {
+template <class LV, class GV>
+__device__ __forceinline__ void help_part_a(const DevPlan &t, int k, const LV &L, const GV &G, float4 *rec, X3 &P, B3 &Gbb) {
 	const int4 sr = t.step_rec[k];
 	const int b = sr.x & 0xffff;
 	const int flags = sr.z & 0xffff;
 	const bool hasP = (flags & mbik::SR_HAS_POSE_PARENT) != 0;
 	P = xid();
 	if (flags & mbik::SR_PARENT_GLOBAL) {
-		P = ld_x(G + 12 * ((sr.y & 0xffff) - 1));
+		P = G.ld((sr.y & 0xffff) - 1);
 		for (int q = (sr.x >> 16) - 2; q > k; q--) P = P * L.ld(t.seg_bones[q]);
 	}
 	const X3 Lb = L.ld(b);
@@ -993,8 +1000,8 @@ __device__ __forceinline__ void qcp_terms(const V3 wc1, const V3 c1, const V3 c2
 // HELP: the parent-side values come from the helper wave's record hrec (kHelpF4 float4 at
 // stride 64), not from this wave.  XS: the build serves split-exchange tasks (xs, staging 4 /
 // 5): only the two-waves-per-SIMD build, so that the one-wave kernels keep their registers.
-template <bool STAB, bool PR, int TA, bool HELP, bool XS, class LV, class FP, class IP>
-__device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j, int m, int xs, size_t s, const LV &L, const FP G, const FP TG,
+template <bool STAB, bool PR, int TA, bool HELP, bool XS, class LV, class GV, class FP, class IP>
+__device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j, int m, int xs, size_t s, const LV &L, const GV &G, const FP TG,
 		const FP ST, const IP SF, const FP HS, const FP OE, const FP MS, double &prev_dev, const EffPre &pre, bool hoist, bool dbh,
 		const float4 *hrec, int *hflB, int hseq, bool *hstuck MBIK_PROF_PARAM) {
 	MBIK_PROF_T(pt0);
@@ -1017,7 +1024,7 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 		// (P, Pinv: read after the wait for the record's part B, below)
 	} else {
 		if (flags & mbik::SR_PARENT_GLOBAL) {
-			P = ld_x(G + 12 * ((sr.y & 0xffff) - 1));
+			P = G.ld((sr.y & 0xffff) - 1);
 			for (int q = (sr.x >> 16) - 2; q > k; q--) P = P * L.ld(t.seg_bones[q]); // none when no checkpoint is skipped
 		}
 		Pinv = inverse(P.b);
@@ -1561,12 +1568,12 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 
 // The same products for the helper wave, whose global pass is the solving wave's wait at each
 // iteration start: the next bone's index and local load before this bone's product and store.
-template <class LV, class FP>
-__device__ void global_pass_pipelined(const DevPlan &t, int seg, const LV &L, const FP G) {
+template <class LV, class GV>
+__device__ void global_pass_pipelined(const DevPlan &t, int seg, const LV &L, const GV &G) {
 	const int kb = t.seg_bone_off[seg], kt = t.seg_bone_off[seg + 1] - 1;
 	int b = t.seg_bones[kt];
 	const int pp = t.bone_pose_parent[b];
-	X3 Gprev = pp >= 0 ? ld_x(G + 12 * t.bone_gslot[pp]) : xid();
+	X3 Gprev = pp >= 0 ? G.ld(t.bone_gslot[pp]) : xid();
 	const bool top_origin = pp == mbik::POSE_PARENT_ORIGIN;
 	X3 Lb = L.ld(b);
 	int gs = t.bone_gslot[b];
@@ -1579,7 +1586,7 @@ __device__ void global_pass_pipelined(const DevPlan &t, int seg, const LV &L, co
 			gn = t.bone_gslot[bn];
 		}
 		const X3 Gb = k < kt ? Gprev * Lb : (pp >= 0 ? Gprev * Lb : (top_origin ? xid() * Lb : Lb));
-		if (gs >= 0) st_x(G + 12 * gs, Gb);
+		if (gs >= 0) G.st(gs, Gb);
 		Gprev = Gb;
 		Lb = Ln;
 		gs = gn;
@@ -1587,8 +1594,8 @@ __device__ void global_pass_pipelined(const DevPlan &t, int seg, const LV &L, co
 }
 
 // Iteration-start globals of one segment, root -> tip (IKNode3D::get_global_transform).
-template <class LV, class FP>
-__device__ void global_pass(const DevPlan &t, int seg, const LV &L, const FP G) {
+template <class LV, class GV>
+__device__ void global_pass(const DevPlan &t, int seg, const LV &L, const GV &G) {
 	X3 Gprev = xid();
 	for (int k = t.seg_bone_off[seg + 1] - 1; k >= t.seg_bone_off[seg]; k--) {
 		const int b = t.seg_bones[k];
@@ -1596,8 +1603,8 @@ __device__ void global_pass(const DevPlan &t, int seg, const LV &L, const FP G) 
 		X3 Lb = L.ld(b);
 		X3 Gb;
 		if (k < t.seg_bone_off[seg + 1] - 1) Gb = Gprev * Lb; // parent = the bone just done
-		else Gb = pp >= 0 ? ld_x(G + 12 * t.bone_gslot[pp]) * Lb : (pp == mbik::POSE_PARENT_ORIGIN ? xid() * Lb : Lb);
-		if (t.bone_gslot[b] >= 0) st_x(G + 12 * t.bone_gslot[b], Gb);
+		else Gb = pp >= 0 ? G.ld(t.bone_gslot[pp]) * Lb : (pp == mbik::POSE_PARENT_ORIGIN ? xid() * Lb : Lb);
+		if (t.bone_gslot[b] >= 0) G.st(t.bone_gslot[b], Gb);
 		Gprev = Gb;
 	}
 }
@@ -1686,21 +1693,27 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 	using FP = std::conditional_t<PL == 2, BPtr<float>, float *>;
 	using IP = std::conditional_t<PL == 2, BPtr<int>, int *>;
 	using LV = std::conditional_t<PL >= 1, LocTiled<FP>, LocContig>;
+	using GV = std::conditional_t<PL == 2, LocTiled<FP>, GFlat<FP>>;
 	LV L;
-	FP G;
+	GV G;
+	FP S0; // the skeleton's state after its locals (placement 2: and after its checkpoint globals)
 	const size_t loc0 = (s / kLocTile) * (size_t)(12 * kLocTile) * B + (s % kLocTile) * 4;
 	if constexpr (PL == 2) L.p = bptr<float>(t.Lg, t.lg_bytes, (uint32_t)(loc0 * sizeof(float)), 0u, t.lg_bytes);
 	else if constexpr (PL == 1) L.p = t.Lg + loc0;
 	if constexpr (PL == 2) {
 		const uint32_t sb = (uint32_t)(s * (size_t)t.state_stride * sizeof(float));
-		G = bptr<float>(t.Sg, t.sg_bytes, sb, sb, sb + (uint32_t)(t.state_stride * sizeof(float)));
+		S0 = bptr<float>(t.Sg, t.sg_bytes, sb, sb, sb + (uint32_t)(t.state_stride * sizeof(float)));
+		const size_t g0 = (s / kLocTile) * (size_t)(12 * kLocTile) * t.n_gck + (s % kLocTile) * 4;
+		G.p = bptr<float>(t.Gg, t.gg_bytes, (uint32_t)(g0 * sizeof(float)), 0u, t.gg_bytes);
 	} else if constexpr (PL == 1) {
-		G = lds + (size_t)g * t.lds_stride;
+		S0 = lds + (size_t)g * t.lds_stride;
+		G.p = S0;
 	} else {
 		L.p = lds + (size_t)g * t.lds_stride;
-		G = L.p + 12 * B;
+		S0 = L.p + 12 * B;
+		G.p = S0;
 	}
-	const FP TG = uplus(G, 12 * t.n_gck, 1);
+	const FP TG = uplus(S0, PL == 2 ? 0 : 12 * t.n_gck, 1);
 	const FP ST = uplus(TG, 12 * P, 2);
 	const FP HS = uplus(ST, 12 * P, 4);               // staged headings (t.seg_hbase), 16-B aligned
 	const IP SF = rebind<int>(uplus(HS, t.hs_floats, 8));
@@ -2037,6 +2050,8 @@ struct mbik_plan {
 	float *d_locals = nullptr;                           // [N][B][12] for state_hbm 1
 	float *d_state = nullptr;                            // [N][state stride] for state_hbm 2
 	size_t d_state_floats = 0;
+	float *d_gtile = nullptr;                            // state_hbm 2: checkpoint globals, skeleton-tiled
+	size_t d_gtile_floats = 0;
 	void *d_sched = nullptr; // topology blob (includes the lane schedule)
 	// scratch for mbik_solve_host
 	float *d_in = nullptr, *d_tg = nullptr, *d_out = nullptr;
@@ -2234,12 +2249,28 @@ int ensure_schedule(mbik_plan *p, int64_t nlaunch) {
 	if (lanes == 0 && h.constraint_mode && h.K > kCmodeLanes)
 		mbik::build_schedule(h, kCmodeLanes, nlaunch, p->spw_override, p->interval_override, blocks_per_cu, p, p->cu_count);
 	if (h.state_hbm == 2) {
-		// the whole state in device memory: one skeleton's LDS layout per skeleton
-		// (the locals live in the tiled area, d_locals)
-		const int stride = (mbik::state_floats_per_skeleton(h) - 12 * h.B + 3) & ~3;
+		// the whole state in device memory: one skeleton's LDS layout per skeleton (the locals
+		// and the checkpoint globals live in skeleton-tiled areas, d_locals and d_gtile)
+		const int stride = (mbik::state_floats_per_skeleton(h) - 12 * h.B - 12 * h.n_gck + 3) & ~3;
 		const size_t need = (size_t)h.N * stride;
-		if (need * sizeof(float) > kMaxBufBytes || p->dev.lg_bytes > kMaxBufBytes)
+		const size_t gneed = (size_t)((h.N + kLocTile - 1) / kLocTile) * kLocTile * (size_t)std::max(1, h.n_gck) * 12;
+		if (need * sizeof(float) > kMaxBufBytes || p->dev.lg_bytes > kMaxBufBytes || gneed * sizeof(float) > kMaxBufBytes)
 			return fail(MBIK_EUNSUPPORTED, "solve state in device memory needs < 4 GiB per area (fewer skeletons per plan)");
+		if (gneed > p->d_gtile_floats) {
+			void *a = nullptr;
+			if (hipMalloc(&a, gneed * sizeof(float)) != hipSuccess) return fail(MBIK_ENOMEM, "hipMalloc checkpoint globals");
+			if (p->d_gtile) {
+				(void)hipFree(p->d_gtile);
+				p->allocs.erase(std::remove(p->allocs.begin(), p->allocs.end(), (void *)p->d_gtile), p->allocs.end());
+				p->device_bytes -= (int64_t)(p->d_gtile_floats * sizeof(float));
+			}
+			p->d_gtile = static_cast<float *>(a);
+			p->d_gtile_floats = gneed;
+			p->allocs.push_back(a);
+			p->device_bytes += (int64_t)(gneed * sizeof(float));
+		}
+		p->dev.Gg = p->d_gtile;
+		p->dev.gg_bytes = (uint32_t)(p->d_gtile_floats * sizeof(float));
 		if (need > p->d_state_floats) {
 			void *a = nullptr;
 			if (hipMalloc(&a, need * sizeof(float)) != hipSuccess) return fail(MBIK_ENOMEM, "hipMalloc state");
