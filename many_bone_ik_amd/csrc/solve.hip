@@ -1637,8 +1637,11 @@ __device__ __forceinline__ void write_nonfinite(const DevPlan &t, bool valid, bo
 #endif
 // The solve of one block (blk = the plan-local block index after the XCD remap).
 // Wave-uniform bone-step count of schedule row r: the longest segment among its tasks (the
-// helper and the solving wave walk the same (row, step) sequence).
+// helper and the solving wave walk the same (row, step) sequence).  For a whole-plan solve it
+// comes precomputed in the row's first task (.w >> 8, upload_topology): the K dependent table
+// reads of the loop below sat in the helper's iteration-start path.
 __device__ __forceinline__ int row_steps(const DevPlan &t, int r, int seg_lo, int seg_hi) {
+	if (seg_lo == 0 && seg_hi >= t.NS - 1) return __builtin_amdgcn_readfirstlane(t.sched[r * t.K].w >> 8);
 	int n = 0;
 	for (int i = 0; i < t.K; i++) {
 		const int sg = t.sched[r * t.K + i].x;
@@ -2127,7 +2130,16 @@ int upload_topology(mbik_plan *p) {
 		if (bytes) std::memcpy(blob.data() + off, data, bytes);
 	};
 	std::vector<int4> rows(h.sched.size());
-	for (size_t i = 0; i < rows.size(); i++) rows[i] = make_int4(h.sched[i].seg, h.sched[i].j, h.sched[i].m, h.sched[i].xs);
+	for (size_t i = 0; i < rows.size(); i++) {
+		// .w: the SCHED_* bits, and above bit 8 the row's longest segment in bone-steps (row_steps)
+		const size_t r0 = i / (size_t)h.K * (size_t)h.K;
+		int nq = 0;
+		for (int l = 0; l < h.K; l++) {
+			const int sg = h.sched[r0 + l].seg;
+			if (sg >= 0) nq = std::max(nq, h.seg_bone_off[sg + 1] - h.seg_bone_off[sg]);
+		}
+		rows[i] = make_int4(h.sched[i].seg, h.sched[i].j, h.sched[i].m, h.sched[i].xs | (nq << 8));
+	}
 	add(rows.data(), rows.size() * sizeof(int4), 4, d.o_sched);
 #define MBIK_ADD(T, name) \
 	if (std::string(#name) != "sched") add(h.name.data(), h.name.size() * sizeof(h.name[0]), sizeof(T) >= 16 ? 4 : (sizeof(T) >= 8 ? 2 : 1), d.o_##name);
