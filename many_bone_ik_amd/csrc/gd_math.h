@@ -131,6 +131,15 @@ GDI GdRcp gd_sqrt_rcp(float l, float &len) {
 //   acosf      sysdeps/ieee754/flt-32/e_acosf.c (fdlibm, float arithmetic, IEEE sqrt/div).
 // mbik_selftest_libm (tests/test_gpu_libm.py) proves the device results equal to the host
 // libm's on all 2^32 inputs; tools/libm_exhaustive.c does the same for the oracle's copy.
+//
+// Third-party notices (THIRD_PARTY_NOTICES.md): the coefficient and 2/pi tables and the
+// algorithms of the sinf/cosf below come from the GNU C Library, Copyright (C) 2018-2022
+// Free Software Foundation, Inc., licensed under the GNU Lesser General Public License
+// v2.1 or later.  acosf follows fdlibm's e_acosf.c: "Copyright (C) 1993 by Sun
+// Microsystems, Inc. All rights reserved. Developed at SunPro, a Sun Microsystems, Inc.
+// business. Permission to use, copy, modify, and distribute this software is freely
+// granted, provided that this notice is preserved." (float conversion by Ian Lance
+// Taylor, Cygnus Support).
 namespace glibc {
 GDI uint32_t top12(float x) { // exponent and top mantissa bits of |x|
 	union {

@@ -22,6 +22,13 @@
  * tools/libm_exhaustive.c checks this file against the platform libm on all 2^32 inputs
  * (profiles/r02_libm_exhaustive.txt).  Build with -ffp-contract=off: every contraction
  * here is written out as fma().
+ *
+ * Third-party notices (THIRD_PARTY_NOTICES.md): sinf/cosf tables and algorithms from the
+ * GNU C Library, Copyright (C) 2018-2022 Free Software Foundation, Inc., LGPL-2.1-or-later.
+ * acosf from fdlibm: Copyright (C) 1993 by Sun Microsystems, Inc. All rights reserved.
+ * Developed at SunPro, a Sun Microsystems, Inc. business. Permission to use, copy, modify,
+ * and distribute this software is freely granted, provided that this notice is preserved.
+ * (Float conversion by Ian Lance Taylor, Cygnus Support.)
  */
 #ifndef MBIK_ORACLE_GLIBC_LIBM_H
 #define MBIK_ORACLE_GLIBC_LIBM_H
