@@ -142,6 +142,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # Rehearsal knobs for a 1-GPU box (never set by the driver): every rank on one device, and
+    # the process-group backend ("nccl" = RCCL by default; "gloo" carries device tensors too).
+    if os.environ.get("MBIK_BENCH_DEVICE"):
+        local_rank = int(os.environ["MBIK_BENCH_DEVICE"])
+    backend = os.environ.get("MBIK_BENCH_BACKEND", "nccl")
     if world != args.gpus:
         sys.exit(f"WORLD_SIZE={world} but --gpus {args.gpus}: one rank per GPU is required")
     if args.dry_run:
@@ -151,7 +156,7 @@ def main():
     if world > 1:
         import torch.distributed as dist_mod
         dist = dist_mod
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        dist.init_process_group(backend, device_id=torch.device("cuda", local_rank))
     dev = torch.device("cuda", local_rank)
 
     from many_bone_ik_amd import workloads as W
@@ -322,6 +327,10 @@ def main():
         "pcie_inclusive": pcie,
         "parity": parity,
     }
+    if world > 1:
+        out["backend"] = backend
+    if os.environ.get("MBIK_BENCH_DEVICE"):
+        out["rehearsal"] = f"all {world} ranks on cuda:{local_rank} (MBIK_BENCH_DEVICE): not a scaling measurement"
     if world == 1 and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds, **flags)
