@@ -307,6 +307,11 @@ def main():
                    "baseline_config": f"configs[{cfg - 1}]",
                    "skeletons_total": total, "skeletons_per_gpu": n, "bones": wl.bone_count, "effectors": int(wl.topo.pins.shape[0]),
                    "cones_per_bone": wl.topo.cones_per_bone, "iterations": wl.topo.iterations,
+                   # bone-steps per iteration on the longest root->leaf path (the latency chain);
+                   # SURVEY §8 sized its spine topology at the second figure (why
+                   # the rig hangs its chains off one root bone instead)
+                   "critical_path_steps": W.critical_path_steps(wl.topo),
+                   "survey_critical_path_steps": W.SURVEY_CRITICAL_PATH[cfg],
                    "lanes_per_skeleton": info["lanes_per_skeleton"], "skeletons_per_block": info["skeletons_per_block"],
                    "lds_bytes_per_block": info["lds_bytes_per_block"],
                    "layout": {k: info[k] for k in ("checkpoint_interval", "heading_staging", "state_placement",

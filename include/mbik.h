@@ -50,7 +50,7 @@ extern "C" {
 #define MBIK_EUNSUPPORTED (-4)
 #define MBIK_ENODEV (-5)
 
-#define MBIK_ABI_VERSION 5
+#define MBIK_ABI_VERSION 6
 
 typedef struct mbik_plan mbik_plan;
 typedef struct mbik_group mbik_group;
@@ -105,7 +105,7 @@ typedef struct mbik_plan_info {
 	double algorithmic_flops_per_skeleton; /* SURVEY.md §8(d) per-bone-step formula x bone-steps x iterations */
 	int64_t lds_bytes_per_block;       /* LDS of one launch block (spw skeletons + topology tables) */
 	int32_t checkpoint_interval;       /* iteration-start globals kept every n-th bone (1 << 20: segment roots only) */
-	int32_t heading_staging;           /* mbik_plan_set_heading_staging in effect (0 .. 3) */
+	int32_t heading_staging;           /* mbik_plan_set_heading_staging in effect (0 .. 5) */
 	int32_t state_placement;           /* mbik_plan_set_locals_placement in effect (0 / 1 / 2) */
 	int32_t waves_per_simd;            /* mbik_plan_set_waves_per_simd in effect (1 / 2) */
 	int32_t constraint_slots;          /* slots of mbik_plan_setup_tables' CF / CD (ABI 3) */
@@ -169,8 +169,18 @@ int32_t mbik_plan_set_layout(mbik_plan *plan, int32_t lanes_per_skeleton, int32_
  * every lane of the group solves the segment alone from registers -- no staging LDS, so
  * more skeletons fit per CU, at a longer step for those segments.  2: only the translating
  * root segments (the ones with the most effectors) are staged; 3: only segments with two or
- * more effectors (whose path walks the lanes split).  -1: automatic
- * (mbik_plan_autotune times them).  Results do not depend on it. */
+ * more effectors (whose path walks the lanes split).
+ * 4: split-exchange -- no segment is staged in memory; the lanes of a multi-effector segment's
+ * group build alternate effectors' headings and read each other's through cross-lane
+ * operations (ds_bpermute), every lane summing all of them in the reference's order; 5: the
+ * translating root segments staged as in 2, the other multi-effector segments split-exchanged
+ * as in 4.  Modes 4 and 5 are served by the two-waves-per-SIMD build only
+ * (mbik_plan_set_waves_per_simd 2): with one wave per SIMD their split-exchange segments are
+ * solved as in 0 (each lane alone); when the setup tables need 64-bit indices
+ * (mbik_plan_set_table_addressing) 4 becomes 0 and 5 becomes 2, which
+ * mbik_plan_info.heading_staging then reports.  -1: automatic (mbik_plan_autotune times them; it picks 4 for the
+ * residency-bound BASELINE configs C3-C5).  Not used by constraint_mode (its lanes own tree
+ * ranges).  Results do not depend on it. */
 int32_t mbik_plan_set_heading_staging(mbik_plan *plan, int32_t staging);
 /* Where the solve keeps its per-skeleton state during a launch: 0 (default) all in LDS;
  * 1 the bone local transforms in a per-skeleton device-memory area (L2-resident; about half
@@ -190,10 +200,27 @@ int32_t mbik_plan_set_waves_per_simd(mbik_plan *plan, int32_t waves);
  * It pays where SIMDs would otherwise idle: launches resident at once with their state in LDS
  * (a frame of BASELINE configs[1]).  Serves state placement 0 without stabilization; other
  * layouts ignore it.  0 off, -1 (default) automatic: off until mbik_plan_autotune has timed
- * it on a fully resident launch.  Results do not depend on it.  Every wait between the two
- * waves has an exit; a wave that took it (an ordering error, never a data-dependent event)
- * is reported as MBIK_EHIP by the synchronous calls (mbik_plan_autotune, mbik_solve_host). */
+ * it on a fully resident launch.  Results do not depend on it.
+ * Every wait between the two waves has an exit: a wait whose counter has not moved for two
+ * seconds (a real wait lasts at most one iteration of the partner) gives up for the rest of
+ * the launch.  The block's skeletons are then written as failures -- identity rotation, NaN
+ * position, unit scale for every solved bone -- with their mbik_solve_checked flag set, and
+ * the plan's own timeout flag is raised (mbik_plan_status).  The synchronous calls
+ * (mbik_solve_host, mbik_plan_autotune) return MBIK_EHIP for their own launch; the
+ * asynchronous ones (mbik_solve, mbik_solve_checked, mbik_segment_solve, mbik_group_solve)
+ * return MBIK_EHIP, without launching, on the plan's next call, which clears the flag.
+ * Plans never see each other's timeouts. */
 int32_t mbik_plan_set_helper_wave(mbik_plan *plan, int32_t helper);
+/* Status of a plan's earlier launches, for callers that poll instead of waiting for the next
+ * call's return code (ABI 6): *status = MBIK_STATUS_HELPER_TIMEOUT when a helper-wave launch of
+ * this plan that has completed timed out (see mbik_plan_set_helper_wave), else 0.  Reading
+ * does not clear it. */
+#define MBIK_STATUS_HELPER_TIMEOUT 1u
+int32_t mbik_plan_status(const mbik_plan *plan, uint32_t *status);
+/* Test hook (ABI 6): the helper wave stops before producing record drop_record of each block
+ * (-1: never), and the handshake deadline is timeout_us microseconds (0: the default two
+ * seconds) -- to exercise the timeout path above.  Not for production use. */
+int32_t mbik_plan_debug_helper(mbik_plan *plan, int32_t drop_record, int32_t timeout_us);
 /* How the solve addresses the per-skeleton setup tables (D, CF, CD).  0 (default): with
  * 32-bit offsets from a buffer resource when every table is below 4 GiB, else with 64-bit
  * element indices.  1: always 64-bit indices (state placement 0 only: placements 1 and 2 need

@@ -30,6 +30,7 @@ EXPORTED_SYMBOLS = (
     "mbik_plan_create", "mbik_plan_create_opts", "mbik_plan_create_device_opts", "mbik_plan_destroy", "mbik_plan_save", "mbik_plan_load", "mbik_plan_get_info", "mbik_plan_set_launch", "mbik_plan_set_layout",
     "mbik_plan_autotune", "mbik_plan_resident_blocks", "mbik_plan_set_heading_staging",
     "mbik_plan_set_locals_placement", "mbik_plan_set_waves_per_simd", "mbik_plan_set_helper_wave", "mbik_plan_set_table_addressing", "mbik_plan_rebuild_setup", "mbik_plan_setup_tables",
+    "mbik_plan_status", "mbik_plan_debug_helper",
     "mbik_solve", "mbik_solve_checked", "mbik_solve_host", "mbik_segment_solve", "mbik_plan_segment_table", "mbik_describe_topology",
     "mbik_group_create", "mbik_group_solve", "mbik_group_destroy", "mbik_capture_targets", "mbik_selftest_math",
     "mbik_selftest_libm", "mbik_selftest_div", "mbik_selftest_topology", "mbik_plan_create_device", "mbik_last_error",
@@ -131,6 +132,11 @@ def load():
     if hasattr(L, "mbik_plan_set_helper_wave"):  # (absent from older A/B builds)
         L.mbik_plan_set_helper_wave.argtypes = [vp, C.c_int32]
         L.mbik_plan_set_helper_wave.restype = C.c_int32
+    if hasattr(L, "mbik_plan_status"):  # (ABI 6; absent from older A/B builds)
+        L.mbik_plan_status.argtypes = [vp, C.POINTER(C.c_uint32)]
+        L.mbik_plan_status.restype = C.c_int32
+        L.mbik_plan_debug_helper.argtypes = [vp, C.c_int32, C.c_int32]
+        L.mbik_plan_debug_helper.restype = C.c_int32
     if hasattr(L, "mbik_plan_set_table_addressing"):  # (absent from older A/B builds, tools/variant_check.py)
         L.mbik_plan_set_table_addressing.argtypes = [vp, C.c_int32]
         L.mbik_plan_set_table_addressing.restype = C.c_int32

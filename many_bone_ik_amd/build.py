@@ -65,5 +65,32 @@ def build(force: bool = False, verbose: bool = False) -> str:
     return OUT
 
 
+# tests/capi_frame.c: a C99 consumer of include/mbik.h (INTEGRATION.md §3's frame loop), linked
+# against the in-tree libmbik.so through an $ORIGIN rpath so the binary travels with the tree.
+CAPI_FRAME_SRC = os.path.join(HERE, "..", "tests", "capi_frame.c")
+CAPI_FRAME = os.path.join(HERE, "..", "tests", "capi_frame")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+
+
+def capi_frame_cmd(out: str = CAPI_FRAME) -> list[str]:
+    return ["gcc", "-std=c99", "-Wall", "-Wextra", "-Werror", "-O2", "-D__HIP_PLATFORM_AMD__",
+            "-I", os.path.join(HERE, "..", "include"), "-I", os.path.join(ROCM, "include"), CAPI_FRAME_SRC,
+            "-L", HERE, "-l:libmbik.so", "-L", os.path.join(ROCM, "lib"), "-lamdhip64",
+            "-Wl,-rpath,$ORIGIN/../many_bone_ik_amd", "-Wl,-rpath," + os.path.join(ROCM, "lib"), "-o", out]
+
+
+def build_capi_frame(verbose: bool = False) -> str:
+    build()
+    src_newer = (not os.path.exists(CAPI_FRAME) or os.path.getmtime(CAPI_FRAME) < max(
+        os.path.getmtime(CAPI_FRAME_SRC), os.path.getmtime(OUT), os.path.getmtime(os.path.join(HERE, "..", "include", "mbik.h"))))
+    if src_newer:
+        cmd = capi_frame_cmd()
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True)
+    return CAPI_FRAME
+
+
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))
+    print(build_capi_frame(verbose=True))

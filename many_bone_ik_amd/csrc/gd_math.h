@@ -24,6 +24,18 @@ using std::isfinite; // a plain C++ compiler (the sanitizer build, tools/san) pu
 using std::isnan;
 #endif
 
+// Timing-only ablation builds: tools/ablate.sh compiles with -DMBIK_ABLATE=<mask of the bits
+// below> to time the solve with one phase removed (the results are wrong on purpose).  The
+// shipped library is built with mask 0, where every `if constexpr (kAblate & ...)` is dead.
+#ifndef MBIK_ABLATE
+#define MBIK_ABLATE 0
+#endif
+enum : unsigned {
+	ABL_SQRT = 1, ABL_ORTHO = 2, ABL_MATMUL = 4, ABL_SOA = 8, ABL_SOALDS = 16, ABL_CONVERT = 32, ABL_SLERP = 64,
+	ABL_SWING = 128, ABL_TWIST = 256, ABL_XCD = 512
+};
+constexpr unsigned kAblate = MBIK_ABLATE;
+
 constexpr double CMP_EPSILON = 0.00001;
 constexpr double PI = 3.1415926535897932384626433833;
 
@@ -32,10 +44,9 @@ constexpr double PI = 3.1415926535897932384626433833;
 // once to float.  tools/sqrt_exhaustive.hip checks all 2^32 inputs against the compiler's
 // correctly rounded sqrtf: identical for every non-NaN result (NaN payloads may differ;
 // NaN-ness does not).  Half the latency of the fp32 sequence (55 vs 107 cycles, same tool).
-#if defined(MBIK_ABLATE_SQRT) && defined(__HIP_DEVICE_COMPILE__)
-GDI float gd_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); } // timing experiment only (1 ulp)
-#elif defined(__HIP_DEVICE_COMPILE__) && !defined(MBIK_IEEE_SQRT)
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(MBIK_IEEE_SQRT)
 GDI float gd_sqrt(float x) {
+	if constexpr (kAblate & ABL_SQRT) return __builtin_amdgcn_sqrtf(x); // timing experiment only (1 ulp)
 	const double xd = x;
 	const double y = __builtin_amdgcn_rsq(xd);
 	const double g = xd * y, h = 0.5 * y;
@@ -339,7 +350,7 @@ GDI float slerp_scale0(float omega, int lv = LIBM_FMA) {
 }
 #endif
 
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(MBIK_NO_PACK)
+#if defined(__HIP_DEVICE_COMPILE__)
 #define GD_PACK 1
 typedef float F2 __attribute__((ext_vector_type(2)));
 #endif
@@ -564,9 +575,7 @@ GDI Q get_quaternion(const B3 &m) {
 }
 // Basis::orthonormalize (Gram-Schmidt on columns)
 GDI B3 orthonormalized(const B3 &b) {
-#ifdef MBIK_ABLATE_ORTHO
-	return b; // timing experiment only
-#endif
+	if constexpr (kAblate & ABL_ORTHO) return b; // timing experiment only
 	V3 x = col(b, 0), y = col(b, 1), z = col(b, 2);
 	x = normalized(x);
 	y = (y - x * dot(x, y));
@@ -599,10 +608,10 @@ GDI B3 inverse(const B3 &b) {
 // Basis::operator*: (A*B)[i][j] = B[0][j]*A[i][0] + B[1][j]*A[i][1] + B[2][j]*A[i][2]
 GDI B3 operator*(const B3 &a, const B3 &b) {
 	B3 r;
-#ifdef MBIK_ABLATE_MATMUL
-	for (int i = 0; i < 3; i++) r.r[i] = a.r[i] * b.r[i].x; // timing experiment only
-	return r;
-#endif
+	if constexpr (kAblate & ABL_MATMUL) {
+		for (int i = 0; i < 3; i++) r.r[i] = a.r[i] * b.r[i].x; // timing experiment only
+		return r;
+	}
 #pragma unroll
 	for (int i = 0; i < 3; i++) {
 		V3 ar = a.r[i];

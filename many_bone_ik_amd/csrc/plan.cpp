@@ -698,7 +698,7 @@ void build_schedule(HostPlan &p, int32_t lanes, int64_t nlaunch, int32_t spw_ove
 		int used = 0;
 		for (int l = 0; l < K; l++) {
 			const SchedTask &tk = p.sched[(size_t)r * K + l];
-			if (tk.seg < 0 || tk.j != 0 || tk.m < 2 || tk.xs || p.seg_nh[tk.seg] < 2) continue;
+			if (tk.seg < 0 || tk.j != 0 || tk.m < 2 || (tk.flags & SCHED_XS) || p.seg_nh[tk.seg] < 2) continue;
 			p.seg_hbase[tk.seg] = used;
 			used += 12 * p.seg_nh[tk.seg] + 24;
 		}

@@ -58,9 +58,9 @@ struct SchedTask {
 	int32_t seg;  // -1 idle
 	int32_t j;    // index of this lane inside the segment's lane group
 	int32_t m;    // lanes in the group (power of two, aligned)
-	int32_t xs;   // bit 0 (SCHED_XS): split-exchange (staging 4/5): the group's lanes build alternate effectors'
-	              // headings and share them through cross-lane reads; every lane sums them all in order (no
-	              // staging memory).  bit 1 (SCHED_CHAIN): this row continues the previous one's packed level
+	int32_t flags; // bit 0 (SCHED_XS): split-exchange (staging 4/5): the group's lanes build alternate effectors'
+	               // headings and share them through cross-lane reads; every lane sums them all in order (no
+	               // staging memory).  bit 1 (SCHED_CHAIN): this row continues the previous one's packed level
 };
 constexpr int32_t SCHED_XS = 1, SCHED_CHAIN = 2;
 

@@ -105,6 +105,13 @@ struct DevPlan {
 	// state_hbm 2: the checkpoint globals, skeleton-tiled like the locals, [N/kLocTile][n_gck][3][kLocTile][4]
 	float *Gg = nullptr;
 	uint32_t gg_bytes = 0;
+	// Helper-wave launches: the plan's timeout flag (host-mapped, one word per plan), set to 1 by
+	// a block whose waves gave up waiting for each other; the wait's deadline in wall-clock ticks
+	// (s_memrealtime, since the awaited counter last moved); and a test hook: the helper stops
+	// before producing record help_drop (-1: never; mbik_plan_debug_helper).
+	unsigned int *help_flag = nullptr;
+	uint64_t help_timeout = 0;
+	int help_drop = -1;
 };
 
 // ------------------------------------------------------------------------------------
@@ -139,10 +146,6 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void *base, uin
 //   MBIK_CHECK_BOUNDS  every buffer-pointer access checks that it stays inside the area it was
 //                      derived from (one skeleton's state slice, or the whole locals area) and
 //                      inside the resource's records; the first violations are printed.
-//   MBIK_SOFF          the wave-uniform distance of a state area from the skeleton's slice
-//                      (TG, ST, HS, SF, OE, MS) goes to the instruction's SGPR offset instead of
-//                      the lane's VGPR offset (the round-2 experiment reverted in 395e810;
-//                      DESIGN.md §10 records why it is not shipped).
 struct BDiag {
 #ifdef MBIK_CHECK_BOUNDS
 	uint32_t lo = 0, hi = 0, n = 0; // [lo, hi): the area; n: the resource's records
@@ -150,38 +153,37 @@ struct BDiag {
 };
 #ifdef MBIK_CHECK_BOUNDS
 __device__ unsigned int g_mbik_oob;
-__device__ __noinline__ void mbik_oob_report(const BDiag &d, uint32_t o, uint32_t so, uint32_t sz, int store) {
+__device__ __noinline__ void mbik_oob_report(const BDiag &d, uint32_t o, uint32_t sz, int store) {
 	const unsigned int k = atomicAdd(&g_mbik_oob, 1u);
 	if (k < 24)
-		printf("mbik OOB %s: block %d lane %d voff %u soff %u size %u area [%u,%u) records %u\n", store ? "store" : "load",
-				(int)blockIdx.x, (int)threadIdx.x, o, so, sz, d.lo, d.hi, d.n);
+		printf("mbik OOB %s: block %d lane %d voff %u size %u area [%u,%u) records %u\n", store ? "store" : "load",
+				(int)blockIdx.x, (int)threadIdx.x, o, sz, d.lo, d.hi, d.n);
 }
-__device__ __forceinline__ void mbik_bcheck(const BDiag &d, uint32_t o, uint32_t so, uint32_t sz, int store) {
-	const uint64_t a = (uint64_t)o + so;
-	if (a < d.lo || a + sz > d.hi || (uint64_t)o >= d.n || a + sz > d.n) mbik_oob_report(d, o, so, sz, store);
+__device__ __forceinline__ void mbik_bcheck(const BDiag &d, uint32_t o, uint32_t sz, int store) {
+	const uint64_t a = o;
+	if (a < d.lo || a + sz > d.hi || a >= d.n || a + sz > d.n) mbik_oob_report(d, o, sz, store);
 }
-#define MBIK_BCHECK(d, o, so, sz, st) mbik_bcheck(d, o, so, sz, st)
+#define MBIK_BCHECK(d, o, sz, st) mbik_bcheck(d, o, sz, st)
 #else
-#define MBIK_BCHECK(d, o, so, sz, st)
+#define MBIK_BCHECK(d, o, sz, st)
 #endif
 template <class T>
 struct BRef {
 	__amdgpu_buffer_rsrc_t r;
-	uint32_t o;  // per-lane byte offset (VGPR)
-	uint32_t so; // wave-uniform byte offset (MBIK_SOFF only; 0 otherwise)
+	uint32_t o; // per-lane byte offset (VGPR)
 	BDiag d;
 	__device__ __forceinline__ operator T() const {
 		static_assert(sizeof(T) == 4 || sizeof(T) == 8, "32- or 64-bit elements");
-		MBIK_BCHECK(d, o, so, sizeof(T), 0);
-		if constexpr (sizeof(T) == 4) return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, o, so, 0));
-		else return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, o, so, 0));
+		MBIK_BCHECK(d, o, sizeof(T), 0);
+		if constexpr (sizeof(T) == 4) return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, o, 0, 0));
+		else return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, o, 0, 0));
 	}
 	__device__ __forceinline__ const BRef &operator=(T v) const {
-		MBIK_BCHECK(d, o, so, sizeof(T), 1);
-		if constexpr (sizeof(T) == 4) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, o, so, 0);
+		MBIK_BCHECK(d, o, sizeof(T), 1);
+		if constexpr (sizeof(T) == 4) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, o, 0, 0);
 		else {
 			typedef unsigned int U2 __attribute__((ext_vector_type(2)));
-			__builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(U2, v), r, o, so, 0);
+			__builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(U2, v), r, o, 0, 0);
 		}
 		return *this;
 	}
@@ -189,20 +191,20 @@ struct BRef {
 template <class T>
 struct BPtr {
 	__amdgpu_buffer_rsrc_t r;
-	uint32_t o, so;
+	uint32_t o;
 	BDiag d;
-	__device__ __forceinline__ BPtr operator+(int i) const { return BPtr{r, o + (uint32_t)(i * (int)sizeof(T)), so, d}; }
+	__device__ __forceinline__ BPtr operator+(int i) const { return BPtr{r, o + (uint32_t)(i * (int)sizeof(T)), d}; }
 	__device__ __forceinline__ BPtr &operator+=(int i) {
 		o += (uint32_t)(i * (int)sizeof(T));
 		return *this;
 	}
-	__device__ __forceinline__ BRef<T> operator[](int i) const { return BRef<T>{r, o + (uint32_t)(i * (int)sizeof(T)), so, d}; }
+	__device__ __forceinline__ BRef<T> operator[](int i) const { return BRef<T>{r, o + (uint32_t)(i * (int)sizeof(T)), d}; }
 };
 // A buffer pointer to `bytes` bytes at base, at byte offset o; [lo, hi) bounds the accesses made
 // through it and its derivatives (MBIK_CHECK_BOUNDS only).
 template <class T>
 __device__ __forceinline__ BPtr<T> bptr(const void *base, uint32_t bytes, uint32_t o, uint32_t lo, uint32_t hi) {
-	BPtr<T> p{buf_rsrc(base, bytes), o, 0u, BDiag{}};
+	BPtr<T> p{buf_rsrc(base, bytes), o, BDiag{}};
 #ifdef MBIK_CHECK_BOUNDS
 	p.d.lo = lo;
 	p.d.hi = hi;
@@ -213,43 +215,19 @@ __device__ __forceinline__ BPtr<T> bptr(const void *base, uint32_t bytes, uint32
 #endif
 	return p;
 }
-// p + k for a wave-uniform k (a state area's distance from the skeleton's slice); `area`
-// selects which areas take the SGPR form under MBIK_SOFF (bit mask MBIK_SOFF, 1 = all).
-#ifdef MBIK_SOFF
-#if MBIK_SOFF == 1
-#define MBIK_SOFF_AREAS 0xFF
-#else
-#define MBIK_SOFF_AREAS MBIK_SOFF
-#endif
-#endif
+// p + k for a wave-uniform k (a state area's distance from the skeleton's slice): the sum
+// stays in the lane's VGPR offset.  (Round 2 tried the instruction's SGPR offset for it and
+// reverted: DESIGN.md §10b.)
 template <class T>
-__device__ __forceinline__ T *uplus(T *p, int k, int area = 0) {
-	(void)area;
-	return p + k;
-}
+__device__ __forceinline__ T *uplus(T *p, int k) { return p + k; }
 template <class T>
-__device__ __forceinline__ BPtr<T> uplus(BPtr<T> p, int k, int area = 0xFF) {
-#ifdef MBIK_SOFF
-	if (area & MBIK_SOFF_AREAS) {
-#ifdef MBIK_SOFF_RFL
-		return BPtr<T>{p.r, p.o, (uint32_t)__builtin_amdgcn_readfirstlane((int)(p.so + (uint32_t)(k * (int)sizeof(T)))), p.d};
-#else
-		return BPtr<T>{p.r, p.o, p.so + (uint32_t)(k * (int)sizeof(T)), p.d};
-#endif
-	}
-#ifdef MBIK_SOFF_STRICT
-	return BPtr<T>{p.r, p.o + p.so + (uint32_t)(k * (int)sizeof(T)), 0u, p.d}; // areas outside the mask: no SGPR part
-#endif
-#endif
-	(void)area;
-	return p + k;
-}
+__device__ __forceinline__ BPtr<T> uplus(BPtr<T> p, int k) { return p + k; }
 // The same element type change for raw and buffer pointers (the staged headings' fp64
 // exchange slots, the int flags after the float state).
 template <class T, class U>
 __device__ __forceinline__ T *rebind(U *p) { return reinterpret_cast<T *>(p); }
 template <class T, class U>
-__device__ __forceinline__ BPtr<T> rebind(BPtr<U> p) { return BPtr<T>{p.r, p.o, p.so, p.d}; }
+__device__ __forceinline__ BPtr<T> rebind(BPtr<U> p) { return BPtr<T>{p.r, p.o, p.d}; }
 // float4 quads through either kind of pointer
 __device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
 __device__ __forceinline__ void st4(float *p, float4 v) { *reinterpret_cast<float4 *>(p) = v; }
@@ -313,13 +291,9 @@ using GFlat = LocV<12, 4, PT>;
 template <class PT>
 using LocTiled = LocV<12 * kLocTile, 4 * kLocTile, PT>;
 // SoA per-skeleton tables: element (item, field) of skeleton s.
-#ifdef MBIK_ABLATE_SOA
-#define MBIK_SOA_S(s) ((s) & 15) // timing experiment only: a hot 16-skeleton working set
-#elif defined(MBIK_ABLATE_SOALDS)
-#define MBIK_SOA_S(s) 0 // timing experiment only: skeleton 0's rows, copied into LDS
-#else
-#define MBIK_SOA_S(s) (s)
-#endif
+// (ablation builds only: ABL_SOA reads a hot 16-skeleton working set, ABL_SOALDS skeleton 0's
+// rows copied into LDS)
+#define MBIK_SOA_S(s) ((kAblate & ABL_SOA) ? ((s) & 15) : (kAblate & ABL_SOALDS) ? 0 : (s))
 constexpr int kRowTile = 16;
 // Table addressing (TA) of a launch:
 //   kTab64    the plan's own layout, 64-bit element indices: tables of any size
@@ -513,13 +487,12 @@ struct EffPre {
 	double hws[7];
 };
 template <int TA, class FP>
-__device__ __forceinline__ void load_eff(const DevPlan &t, int e, const FP TG, size_t s, const double *hw, EffPre &p,
-		const B3 *Db = nullptr) {
+__device__ __forceinline__ void load_eff(const DevPlan &t, int e, const FP TG, size_t s, const double *hw, EffPre &p) {
 	p.e = e;
 	p.off = t.eff_path_off[e];
 	p.de = t.eff_path_off[e + 1] - p.off - 1;
 	p.T = ld_x(TG + 12 * e);
-	p.Db = Db ? *Db : ld_soa_basis<TA>(t, t.D, t.eff_bone[e], 9, 0, s);
+	p.Db = ld_soa_basis<TA>(t, t.D, t.eff_bone[e], 9, 0, s);
 	p.hws[0] = hw[0];
 	int k = 1;
 #pragma unroll
@@ -565,11 +538,6 @@ struct PathCk {
 	X3 x;
 	int d;
 };
-#ifdef MBIK_FAN_RESET
-constexpr bool kFanKeep = false; // A/B switch: round 2's reset after every reuse
-#else
-constexpr bool kFanKeep = true;
-#endif
 template <class LV, class FP, class IP>
 __device__ __forceinline__ void effector_headings(const DevPlan &t, const EffPre &p, int d0, const X3 &Gb, const LV &L,
 		const FP ST, const IP SF, Headings &H, const FP OE, int oe_mode = 0, PathCk *pc = nullptr, const int *lcp = nullptr) {
@@ -586,18 +554,6 @@ __device__ __forceinline__ void effector_headings(const DevPlan &t, const EffPre
 		// loads during the current product
 		auto walk = [&](int a, int b) {
 			if (a > b) return;
-#ifdef MBIK_WALK2
-			// (A/B: two path bones ahead)
-			X3 Ln = L.ld(t.eff_path[off + a]);
-			X3 Lm = a < b ? L.ld(t.eff_path[off + a + 1]) : Ln;
-			for (int d = a; d < b; d++) {
-				const X3 Lc = Ln;
-				Ln = Lm;
-				if (d + 2 <= b) Lm = L.ld(t.eff_path[off + d + 2]);
-				X = X * Lc;
-			}
-			X = X * Ln;
-#else
 			X3 Ln = L.ld(t.eff_path[off + a]);
 			for (int d = a; d < b; d++) {
 				const X3 Lc = Ln;
@@ -605,7 +561,6 @@ __device__ __forceinline__ void effector_headings(const DevPlan &t, const EffPre
 				X = X * Lc;
 			}
 			X = X * Ln;
-#endif
 		};
 		int d = d0;
 		if (pc) {
@@ -620,7 +575,7 @@ __device__ __forceinline__ void effector_headings(const DevPlan &t, const EffPre
 			}
 			// A fan of three or more effectors branching at one depth: the next one shares
 			// exactly the prefix just reused, so the checkpoint stays for it.
-			if (!(kFanKeep && reused && cpd == d - 1)) {
+			if (!(reused && cpd == d - 1)) {
 				pc->d = -1;
 				if (cpd >= d && cpd <= de) {
 					walk(d, cpd);
@@ -645,9 +600,9 @@ __device__ __forceinline__ void effector_headings(const DevPlan &t, const EffPre
 template <int TA, class LV, class FP, class IP>
 __device__ __forceinline__ void effector_headings(const DevPlan &t, int e, int d0, const X3 &Gb, const LV &L,
 		const FP TG, const FP ST, const IP SF, size_t s, const double *hw, Headings &H, const FP OE,
-		int oe_mode = 0, const B3 *Db = nullptr, PathCk *pc = nullptr, const int *lcp = nullptr) {
+		int oe_mode = 0, PathCk *pc = nullptr, const int *lcp = nullptr) {
 	EffPre p;
-	load_eff<TA>(t, e, TG, s, hw, p, Db);
+	load_eff<TA>(t, e, TG, s, hw, p);
 	effector_headings(t, p, d0, Gb, L, ST, SF, H, OE, oe_mode, pc, lcp);
 }
 
@@ -738,44 +693,14 @@ __device__ __forceinline__ V3 great_tangent_triangle(V3 c1xc2, V3 a1, V3 a2, V3 
 	return v3(NAN, NAN, NAN);
 }
 
-#ifdef MBIK_NO_PATH_REUSE
-constexpr bool kPathReuse = false; // A/B switch
-#else
-constexpr bool kPathReuse = true;
-#endif
 // The two-wave build used to hold a single-effector segment's bone-direction basis across the
 // segment (round 1: C3 -2 %).  With the state addressing and path sharing of round 2 those nine
 // registers spilled instead (placement 2: 31 spilled registers with them, 22 without), and
-// reading the basis at each step is faster: C3 -1 %, C4 -1.6 %, C5 -3 % (same-box A/B).
-#ifdef MBIK_NO_EFF_HOIST
-constexpr bool kEffHoist = false; // A/B switch: the one-wave build's per-segment effector data
-#else
-constexpr bool kEffHoist = true;
-#endif
-#ifdef MBIK_DBH
-constexpr bool kDbh = true; // A/B switch
-#else
-constexpr bool kDbh = false;
-#endif
-#ifdef MBIK_NO_PR_PL2
-constexpr bool kNoPrPl2 = true;
-#else
-constexpr bool kNoPrPl2 = false;
-#endif
-#ifdef MBIK_PATH_REUSE_2W
-constexpr bool kPathReuse2W = true; // the two-wave build as well (A/B)
-#else
-constexpr bool kPathReuse2W = false;
-#endif
-#ifndef MBIK_STEP_ATTR
-#define MBIK_STEP_ATTR
-#endif
-#ifndef MBIK_LIMITS_ATTR
-#define MBIK_LIMITS_ATTR
-#endif
+// reading the basis at each step is faster: C3 -1 %, C4 -1.6 %, C5 -3 % (same-box A/B).  The
+// one-wave build keeps the whole per-segment effector data (`hoist` in solve_block).
 // IKKusudama3D::get_local_point_in_limits (ik_kusudama_3d.cpp:273-332)
 template <int TA = kTab64>
-__device__ MBIK_LIMITS_ATTR V3 local_point_in_limits(const DevPlan &t, int slot, size_t s, V3 in_point, double &in_bounds) {
+__device__ V3 local_point_in_limits(const DevPlan &t, int slot, size_t s, V3 in_point, double &in_bounds) {
 	const int nc = t.cons_ncones[slot];
 	V3 point = normalized(in_point);
 	float closest_cos = -2.0f;
@@ -841,9 +766,6 @@ __device__ __forceinline__ void wave_sync_lds() {
 	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 	__builtin_amdgcn_wave_barrier();
 	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#ifdef MBIK_SYNC_CLOBBER
-	asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // diagnostic: a hard ordering point
-#endif
 }
 // ---- Helper wave (HELP, fully resident placement-0 launches) ----
 // A bone-step's parent-side work depends only on the iteration-start state: the parent's global
@@ -858,9 +780,10 @@ __device__ __forceinline__ void wave_sync_lds() {
 // Same operations on the same inputs: the record's values are the bits the solving wave would
 // have computed.  Ring: kHelpSlots records of kHelpF4 float4 per lane, [slot][field][64 lanes];
 // four LDS counters (part A produced, part B produced, records consumed, iterations finished)
-// order the two waves.
+// order the two waves; a fifth word is set when either wave gave up waiting (help_wait).
 constexpr int kHelpF4 = 18, kHelpSlots = 4;
-constexpr int kHelpRingBytes = kHelpSlots * kHelpF4 * 64 * 16 + 16;
+constexpr int kHelpRingBytes = kHelpSlots * kHelpF4 * 64 * 16 + 32;
+enum HelpCounter { HC_A = 0, HC_B = 1, HC_CONSUMED = 2, HC_ITER = 3, HC_STUCK = 4 };
 enum HelpField { HF_P = 0, HF_GB = 12, HF_PINV = 24, HF_PNP = 33, HF_STO = 36, HF_HC = 43, HF_DB = 44, HF_GTC = 53, HF_GTCI = 62 };
 __device__ __forceinline__ float hrf(const float4 *r, int i) { return reinterpret_cast<const float *>(r + (i >> 2) * 64)[i & 3]; }
 __device__ __forceinline__ V3 hrv(const float4 *r, int i) { return v3(hrf(r, i), hrf(r, i + 1), hrf(r, i + 2)); }
@@ -868,39 +791,53 @@ __device__ __forceinline__ B3 hrb(const float4 *r, int i) { return B3{{hrv(r, i)
 __device__ __forceinline__ X3 hrx(const float4 *r, int i) { return X3{hrb(r, i), hrv(r, i + 9)}; }
 __device__ __forceinline__ void hw_v(float *f, int i, V3 v) { f[i] = v.x; f[i + 1] = v.y; f[i + 2] = v.z; }
 __device__ __forceinline__ void hw_b(float *f, int i, const B3 &b) { hw_v(f, i, b.r[0]); hw_v(f, i + 3, b.r[1]); hw_v(f, i + 6, b.r[2]); }
-// Waits until counter *f reaches v.  Every wait has an exit: after ~2^22 polls (a fraction of
-// a second; a real wait lasts at most a few bone-steps) the wave stops waiting for the rest of
-// the launch and counts itself in g_mbik_help_stuck (the results are then wrong, and the
-// kernel still drains instead of hanging the GPU).
-__device__ unsigned int g_mbik_help_stuck;
-__device__ __forceinline__ void help_wait(int *f, int v, bool &stuck) {
+// Waits until counter hfl[k] reaches v.  Every wait has an exit: when the counter has not
+// moved for `timeout` wall-clock ticks (a couple of seconds; a real wait lasts at most one
+// iteration of the partner wave) the wave stops waiting for the rest of the launch and raises
+// hfl[HC_STUCK].  The kernel then drains instead of hanging the GPU, and the solving wave writes
+// its skeletons as failed (write_help_timeout): flagged non-finite, the plan's timeout flag set.
+__device__ __forceinline__ void help_give_up(int *hfl, bool &stuck) {
+	stuck = true;
+	__hip_atomic_store(hfl + HC_STUCK, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ bool help_expired(uint64_t &t0, int &seen, int now_val, uint64_t timeout) {
+	const uint64_t now = (uint64_t)wall_clock64();
+	if (t0 == 0 || now_val != seen) {
+		t0 = now;
+		seen = now_val;
+		return false;
+	}
+	return now - t0 > timeout;
+}
+__device__ __forceinline__ void help_wait(int *hfl, int k, int v, bool &stuck, uint64_t timeout) {
 	if (stuck) return;
-	for (int n = 0; __builtin_amdgcn_readfirstlane(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) < v; n++) {
-		if (n >= (1 << 22)) {
-			stuck = true;
-			if ((threadIdx.x & 63) == 0) atomicAdd(&g_mbik_help_stuck, 1u);
-			return;
-		}
+	uint64_t t0 = 0;
+	int seen = 0;
+	for (;;) {
+		const int c = __builtin_amdgcn_readfirstlane(__hip_atomic_load(hfl + k, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+		if (c >= v) return;
+		if (help_expired(t0, seen, c, timeout)) return help_give_up(hfl, stuck);
 		__builtin_amdgcn_s_sleep(1);
 	}
 }
 // The solving wave's wait for record v - 1: counters [0] part A and [1] part B in one 64-bit
 // read; b_ready tells whether part B is already there too (then bone_step skips its wait).
-__device__ __forceinline__ void help_wait_ab(int *f, int v, bool &stuck, bool &b_ready) {
+__device__ __forceinline__ void help_wait_ab(int *hfl, int v, bool &stuck, bool &b_ready, uint64_t timeout) {
 	b_ready = stuck;
 	if (stuck) return;
-	unsigned long long *f2 = reinterpret_cast<unsigned long long *>(f);
-	for (int n = 0;; n++) {
+	unsigned long long *f2 = reinterpret_cast<unsigned long long *>(hfl);
+	uint64_t t0 = 0;
+	int seen = 0;
+	for (;;) {
 		const unsigned long long ab = __hip_atomic_load(f2, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
 		const int a = __builtin_amdgcn_readfirstlane((int)(uint32_t)ab), b = __builtin_amdgcn_readfirstlane((int)(uint32_t)(ab >> 32));
 		if (a >= v) {
 			b_ready = b >= v;
 			return;
 		}
-		if (n >= (1 << 22)) {
-			stuck = b_ready = true;
-			if ((threadIdx.x & 63) == 0) atomicAdd(&g_mbik_help_stuck, 1u);
-			return;
+		if (help_expired(t0, seen, a, timeout)) {
+			b_ready = true;
+			return help_give_up(hfl, stuck);
 		}
 		__builtin_amdgcn_s_sleep(1);
 	}
@@ -1001,9 +938,9 @@ __device__ __forceinline__ void qcp_terms(const V3 wc1, const V3 c1, const V3 c2
 // stride 64), not from this wave.  XS: the build serves split-exchange tasks (xs, staging 4 /
 // 5): only the two-waves-per-SIMD build, so that the one-wave kernels keep their registers.
 template <bool STAB, bool PR, int TA, bool HELP, bool XS, class LV, class GV, class FP, class IP>
-__device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j, int m, int xs, size_t s, const LV &L, const GV &G, const FP TG,
-		const FP ST, const IP SF, const FP HS, const FP OE, const FP MS, double &prev_dev, const EffPre &pre, bool hoist, bool dbh,
-		const float4 *hrec, int *hflB, int hseq, bool *hstuck MBIK_PROF_PARAM) {
+__device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, int xs, size_t s, const LV &L, const GV &G, const FP TG,
+		const FP ST, const IP SF, const FP HS, const FP OE, const FP MS, double &prev_dev, const EffPre &pre, bool hoist,
+		const float4 *hrec, int *hfl, int hseq, bool *hstuck MBIK_PROF_PARAM) {
 	MBIK_PROF_T(pt0);
 #ifdef MBIK_PROF
 	uint64_t pt1 = pt0, pt3 = pt0;
@@ -1057,7 +994,7 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 	if (nh == 1) {
 		// one heading in the segment: every lane of the group computes it (qcp.cpp:59-78)
 		if (hoist) effector_headings(t, pre, d0, Gb, L, ST, SF, H, OE, oe_mode);
-		else effector_headings<TA>(t, t.seg_effs[e0], d0, Gb, L, TG, ST, SF, s, hw, H, OE, oe_mode, dbh ? &pre.Db : nullptr);
+		else effector_headings<TA>(t, t.seg_effs[e0], d0, Gb, L, TG, ST, SF, s, hw, H, OE, oe_mode);
 		V3 mvd = H.hm[0], tgt = H.ht[0];
 		if (translate) {
 			double w = H.w[0];
@@ -1098,7 +1035,7 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 						for (int u = i + 2; u <= i + m; u++) lc[1] = min(lc[1], t.seg_eff_lcp[u]);
 					}
 					effector_headings<TA>(t, t.seg_effs[i], d0, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], Hm, OE, oe_mode,
-							dbh ? &pre.Db : nullptr, PR ? &pc : nullptr, lc);
+							PR ? &pc : nullptr, lc);
 				}
 				for (int v = 0; v < m && i0 + v < e1; v++) {
 					Headings H; // (weights and mask only)
@@ -1163,7 +1100,7 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 			for (int i = e0; i < e1; i++) {
 				if (hoist) effector_headings(t, pre, d0, Gb, L, ST, SF, H, OE, oe_mode);
 				else effector_headings<TA>(t, t.seg_effs[i], d0, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, oe_mode,
-						dbh ? &pre.Db : nullptr, PR ? &pc : nullptr, t.seg_eff_lcp + i);
+						PR ? &pc : nullptr, t.seg_eff_lcp + i);
 #pragma unroll
 				for (int h = 0; h < 7; h++) {
 					if (H.mask & (1 << h)) {
@@ -1187,7 +1124,7 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 			MBIK_PROF_T(ph1);
 			if (hoist) effector_headings(t, pre, d0, Gb, L, ST, SF, H, OE, oe_mode);
 			else effector_headings<TA>(t, t.seg_effs[i], d0, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, oe_mode,
-					dbh ? &pre.Db : nullptr, PR ? &pc : nullptr, t.seg_eff_lcp + i);
+					PR ? &pc : nullptr, t.seg_eff_lcp + i);
 			MBIK_PROF_T(ph2);
 			MBIK_PROF_ADD(9, ph1, ph2);
 #pragma unroll
@@ -1386,7 +1323,7 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 
 	if constexpr (HELP) {
 		MBIK_PROF_T(hb0);
-		if (hflB) help_wait(hflB, hseq + 1, *hstuck);
+		if (hfl) help_wait(hfl, HC_B, hseq + 1, *hstuck, t.help_timeout);
 		MBIK_PROF_T(hb1);
 		MBIK_PROF_ADD(19, hb0, hb1);
 		P = hrx(hrec, HF_P);
@@ -1400,16 +1337,10 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 	MBIK_PROF_ADD(1, pt0, pt1);
 	// ---- damp clamp, slerp(…, 0), rotate, translate, set_global_pose (:144-154) ----
 	const double chd = t.seg_cos_half_damp[k];
-#ifdef MBIK_ABLATE_CONVERT
-	B3 rot = from_quat(qrot);
-#else
-	B3 rot = from_quat(clamp_cos_half(get_rotation_quaternion(from_quat(qrot)), chd));
-#endif
+	B3 rot = (kAblate & ABL_CONVERT) ? from_quat(qrot) : from_quat(clamp_cos_half(get_rotation_quaternion(from_quat(qrot)), chd));
 	MBIK_PROF_T(pc0);
 	MBIK_PROF_ADD(11, pt1, pc0);
-#ifndef MBIK_ABLATE_SLERP
-	rot = slerp_weight0(rot, sto, t.libm);
-#endif
+	if constexpr (!(kAblate & ABL_SLERP)) rot = slerp_weight0(rot, sto, t.libm);
 	MBIK_PROF_T(pc1);
 	MBIK_PROF_ADD(12, pc0, pc1);
 	if (hasP) Lb.b = ((Pinv * rot) * P.b) * Lb.b;
@@ -1441,11 +1372,7 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 	X3 Gbd_stale;
 	B3 GsB = {};     // P.basis * Lb.basis after the swing check, reused by the twist if not swung
 	bool gs_ok = false;
-#ifdef MBIK_ABLATE_SWING
-	if (false) {
-#else
-	if (flags & mbik::BF_ORIENT) {
-#endif
+	if (!(kAblate & ABL_SWING) && (flags & mbik::BF_ORIENT)) {
 		X3 Gs = P * Lb;
 		GsB = Gs.b;
 		gs_ok = true;
@@ -1468,11 +1395,7 @@ __device__ MBIK_STEP_ATTR void bone_step(const DevPlan &t, int seg, int k, int j
 	MBIK_PROF_ADD(3, pt2, pt3);
 	// ---- Kusudama: twist snap (ik_kusudama_3d.cpp:117-132) ----
 	bool twist_changed = false;
-#ifdef MBIK_ABLATE_TWIST
-	if (false) {
-#else
-	if (flags & mbik::BF_AXIAL) {
-#endif
+	if (!(kAblate & ABL_TWIST) && (flags & mbik::BF_AXIAL)) {
 		B3 gtc, gtci;
 		float half_cos;
 		if constexpr (HELP) {
@@ -1622,6 +1545,16 @@ __device__ bool write_pose(const X3 &t, float *out) {
 	out[7] = sc.x; out[8] = sc.y; out[9] = sc.z;
 	return bad;
 }
+// A skeleton of a block whose helper-wave handshake timed out (help_wait): its solve used
+// unfinished records, so every solved bone is written as a failure -- identity rotation, as
+// for a non-finite basis (ik_bone_3d.cpp:174-176), NaN position so the result cannot pass for
+// a pose, unit scale -- and the skeleton is flagged non-finite (mbik_solve_checked).
+__device__ __forceinline__ bool write_help_timeout(float *out) {
+	out[0] = 0.0f; out[1] = 0.0f; out[2] = 0.0f; out[3] = 1.0f;
+	out[4] = NAN; out[5] = NAN; out[6] = NAN;
+	out[7] = 1.0f; out[8] = 1.0f; out[9] = 1.0f;
+	return true;
+}
 // The skeleton's non-finite flag: OR over the K lanes of its group, written by lane role 0.
 __device__ __forceinline__ void write_nonfinite(const DevPlan &t, bool valid, bool bad, int g, int role, int local) {
 	if (!t.nonfinite) return;
@@ -1671,8 +1604,7 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 	MBIK_TOPO_TABLES(MBIK_REPOINT)
 #undef MBIK_REPOINT
 	float *lds = reinterpret_cast<float *>(lds4) + t.topo_words;
-#ifdef MBIK_ABLATE_SOALDS
-	{
+	if constexpr (kAblate & ABL_SOALDS) {
 		float *dl = lds + (size_t)t.spw * t.lds_stride;
 		float *cl = dl + t.B * 9;
 		double *xl = reinterpret_cast<double *>(cl + ((t.NC * t.cf_stride + 1) & ~1));
@@ -1681,7 +1613,6 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 		for (int i = lane; i < t.NC * t.cd_stride; i += 64) xl[i] = t.CD[(size_t)i * t.N + first];
 		t.D = dl; t.CF = cl; t.CD = xl; t.N = 1;
 	}
-#endif
 	const int g = lane >> t.log2K;
 	const int role = lane & (t.K - 1);
 	const int local = blk * t.spw + g;
@@ -1716,13 +1647,13 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 		S0 = L.p + 12 * B;
 		G.p = S0;
 	}
-	const FP TG = uplus(S0, PL == 2 ? 0 : 12 * t.n_gck, 1);
-	const FP ST = uplus(TG, 12 * P, 2);
-	const FP HS = uplus(ST, 12 * P, 4);               // staged headings (t.seg_hbase), 16-B aligned
-	const IP SF = rebind<int>(uplus(HS, t.hs_floats, 8));
+	const FP TG = uplus(S0, PL == 2 ? 0 : 12 * t.n_gck);
+	const FP ST = uplus(TG, 12 * P);
+	const FP HS = uplus(ST, 12 * P);               // staged headings (t.seg_hbase), 16-B aligned
+	const IP SF = rebind<int>(uplus(HS, t.hs_floats));
 	constexpr int TA = PL == 2 ? kTabTiled : (T32 ? kTab32 : kTab64); // placement 2 reads the tiled table copy
-	const FP OE = rebind<float>(uplus(SF, P, 16));    // stabilization only: 3 per pin
-	const FP MS = uplus(OE, 3 * P, 32);              // stabilization only: 7 per pin
+	const FP OE = rebind<float>(uplus(SF, P));    // stabilization only: 3 per pin
+	const FP MS = uplus(OE, 3 * P);              // stabilization only: 7 per pin
 	if (valid && wave == 0) {
 		for (int b = role; b < B; b += K)
 			if (t.bone_flags[b] & mbik::BF_IN_LIST) L.st(b, pose_to_xform(pose_in + ((size_t)local * B + b) * 10));
@@ -1733,11 +1664,12 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 		}
 	}
 	float4 *ring = nullptr;
-	int *hfl = nullptr; // [0] records produced (part A), [1] part B produced, [2] consumed, [3] iterations finished
+	int *hfl = nullptr; // HelpCounter: records produced (part A, part B), consumed, iterations finished, gave up
+	bool help_stuck = false; // this block's waves gave up waiting for each other (help_wait)
 	if constexpr (HELP) {
 		ring = reinterpret_cast<float4 *>(lds + (size_t)t.spw * t.lds_stride) + lane;
 		hfl = reinterpret_cast<int *>(reinterpret_cast<float4 *>(lds + (size_t)t.spw * t.lds_stride) + kHelpSlots * kHelpF4 * 64);
-		if (threadIdx.x < 4) hfl[threadIdx.x] = 0;
+		if (threadIdx.x < 8) hfl[threadIdx.x] = 0;
 	}
 	__syncthreads();
 	MBIK_PROF_T(pk1);
@@ -1754,7 +1686,7 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 			const bool act0 = valid && task0.x >= seg_lo && task0.x <= seg_hi;
 			for (int it = 0; it < iterations; it++) {
 				const HelpRows first_rows = help_rows<kTab32>(t, act0 ? t.seg_bone_off[task0.x] : 0, s);
-				help_wait(hfl + 3, it, stuck);
+				help_wait(hfl, HC_ITER, it, stuck, t.help_timeout);
 				MBIK_PROF_T(hg0);
 				for (int r = t.nrows - 1; r >= 0; r--) {
 					const int4 task = t.sched[r * K + role];
@@ -1770,7 +1702,8 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 					const int nq = row_steps(t, r, seg_lo, seg_hi);
 					for (int q = 0; q < nq; q++, seq++) {
 						const HelpRows rw = (r == 0 && q == 0) ? first_rows : help_rows<kTab32>(t, k0 + q < k1 ? k0 + q : 0, s);
-						help_wait(hfl + 2, seq - kHelpSlots + 1, stuck);
+						if (seq == t.help_drop) return; // test hook (mbik_plan_debug_helper): a helper that dies
+						help_wait(hfl, HC_CONSUMED, seq - kHelpSlots + 1, stuck, t.help_timeout);
 						float4 *rec = ring + slot * (kHelpF4 * 64);
 						X3 P;
 						B3 Gbb;
@@ -1806,20 +1739,20 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 				double prev_dev = INFINITY;
 				const int e0 = t.seg_eff_off[seg];
 				EffPre pre;
-				const bool hoist = act && kEffHoist && t.seg_eff_off[seg + 1] - e0 == 1 && (task.z == 1 || t.seg_nh[seg] == 1);
+				const bool hoist = act && t.seg_eff_off[seg + 1] - e0 == 1 && (task.z == 1 || t.seg_nh[seg] == 1);
 				if (hoist) load_eff<kTab32>(t, t.seg_effs[e0], TG, s, t.seg_hw + t.seg_hw_off[seg] + t.seg_eff_hoff[e0], pre);
 				for (int q = 0; q < nq; q++, seq++) {
 					MBIK_PROF_T(hw0);
 					bool b_ready;
-					help_wait_ab(hfl, seq + 1, stuck, b_ready);
+					help_wait_ab(hfl, seq + 1, stuck, b_ready, t.help_timeout);
 					MBIK_PROF_T(hw1);
 					MBIK_PROF_ADD(18, hw0, hw1);
 #ifdef MBIK_PROF
 					if (r == 0 && q == 0) MBIK_PROF_ADD(20, hw0, hw1);
 #endif
 					if (k0 + q < k1)
-						bone_step<false, kPathReuse, kTab32, true, false>(t, seg, k0 + q, task.y, task.z, task.w & mbik::SCHED_XS, s, L, G, TG, ST, SF, HS, OE, MS, prev_dev,
-								pre, hoist, false, ring + slot * (kHelpF4 * 64), b_ready ? nullptr : hfl + 1, seq, &stuck MBIK_PROF_ARG);
+						bone_step<false, true, kTab32, true, false>(t, seg, k0 + q, task.y, task.z, task.w & mbik::SCHED_XS, s, L, G, TG, ST, SF, HS, OE, MS, prev_dev,
+								pre, hoist, ring + slot * (kHelpF4 * 64), b_ready ? nullptr : hfl, seq, &stuck MBIK_PROF_ARG);
 					help_post(hfl + 2, seq + 1);
 					slot = slot + 1 == kHelpSlots ? 0 : slot + 1;
 				}
@@ -1827,6 +1760,9 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 			}
 			help_post(hfl + 3, it + 1);
 		}
+		// (the helper raises HC_STUCK before any record it writes without waiting, so a record
+		// this wave read from an overwritten slot is covered by the flag read here)
+		help_stuck = stuck || __builtin_amdgcn_readfirstlane(__hip_atomic_load(hfl + HC_STUCK, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) != 0;
 	} else
 	for (int it = 0; it < iterations; it++) {
 		MBIK_PROF_T(pg0);
@@ -1846,7 +1782,7 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 			int4 task = make_int4(-1, 0, 1, 0);
 			double prev_dev = INFINITY;
 			EffPre pre;
-			bool hoist = false, dbh = false;
+			bool hoist = false;
 			for (;;) {
 				while (k >= ke && rr + 1 < r1) {
 					task = t.sched[++rr * K + role];
@@ -1860,17 +1796,13 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 						// (not in the two-waves-per-SIMD build: the hoisted data's ~66 registers are
 						// what push that build past 256 and into scratch spills)
 						const int e0 = t.seg_eff_off[seg];
-						hoist = HOIST && kEffHoist && !STAB && t.seg_eff_off[seg + 1] - e0 == 1 && (task.z == 1 || t.seg_nh[seg] == 1);
+						hoist = HOIST && !STAB && t.seg_eff_off[seg + 1] - e0 == 1 && (task.z == 1 || t.seg_nh[seg] == 1);
 						if (hoist) load_eff<TA>(t, t.seg_effs[e0], TG, s, t.seg_hw + t.seg_hw_off[seg] + t.seg_eff_hoff[e0], pre);
-						// (kDbh: the two-wave build may hoist only the effector's bone-direction basis;
-						// off by default since round 2, see kDbh)
-						dbh = kDbh && !HOIST && !STAB && t.seg_eff_off[seg + 1] - e0 == 1;
-						if (dbh) pre.Db = ld_soa_basis<TA>(t, t.D, t.eff_bone[t.seg_effs[e0]], 9, 0, s);
 					}
 				}
 				if (k >= ke) break;
-				bone_step<STAB, kPathReuse && (HOIST || (PL == 2 && !kNoPrPl2) || kPathReuse2W), TA, false, XS>(t, seg, k, task.y, task.z,
-						task.w & mbik::SCHED_XS, s, L, G, TG, ST, SF, HS, OE, MS, prev_dev, pre, hoist, dbh, nullptr, nullptr, 0, nullptr MBIK_PROF_ARG);
+				bone_step<STAB, HOIST || PL == 2, TA, false, XS>(t, seg, k, task.y, task.z,
+						task.w & mbik::SCHED_XS, s, L, G, TG, ST, SF, HS, OE, MS, prev_dev, pre, hoist, nullptr, nullptr, 0, nullptr MBIK_PROF_ARG);
 				k++;
 			}
 			__syncthreads();
@@ -1883,7 +1815,8 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 		for (int b = role; b < B; b += K) {
 			float *dst = pose_out + ((size_t)local * B + b) * 10;
 			if (t.bone_flags[b] & mbik::BF_IN_LIST) {
-				bad |= write_pose(L.ld(b), dst);
+				if (help_stuck) bad = write_help_timeout(dst);
+				else bad |= write_pose(L.ld(b), dst);
 			} else {
 				const float *src = pose_in + ((size_t)local * B + b) * 10;
 				for (int f = 0; f < 10; f++) dst[f] = src[f];
@@ -1891,6 +1824,7 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 		}
 	}
 	write_nonfinite(t, valid, bad, g, role, local);
+	if (help_stuck && lane == 0 && t.help_flag) __hip_atomic_store(t.help_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 	MBIK_PROF_T(pk3);
 	MBIK_PROF_ADD(6, pk2, pk3);
 	MBIK_PROF_ADD(7, pk0, pk3);
@@ -1905,12 +1839,8 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 // neighbouring skeletons then share cache lines in one L2 instead of eight.
 __device__ __forceinline__ int xcd_block() {
 	const int nb = gridDim.x, nb8 = nb & ~7, bx = blockIdx.x;
-#ifdef MBIK_ABLATE_XCD
-	(void)nb8;
-	return bx;
-#else
+	if constexpr (kAblate & ABL_XCD) return bx;
 	return bx < nb8 ? (bx & 7) * (nb8 >> 3) + (bx >> 3) : bx;
-#endif
 }
 
 // WPE: waves per SIMD the register budget is sized for.  1 (the default): the whole register
@@ -2083,6 +2013,11 @@ struct mbik_plan {
 	hipEvent_t tile_ev = nullptr;
 	hipStream_t tile_stream = nullptr;
 	bool tile_pending = false;
+	// helper-wave timeouts (DevPlan::help_flag): the plan's own host-mapped flag word, which a
+	// launch's kernel sets and the plan's next call reports (take_helper_timeout); the deadline
+	// override of mbik_plan_debug_helper (0: kHelpTimeoutMs)
+	unsigned int *help_flag = nullptr;
+	int help_timeout_us = 0;
 };
 
 namespace {
@@ -2138,7 +2073,7 @@ int upload_topology(mbik_plan *p) {
 			const int sg = h.sched[r0 + l].seg;
 			if (sg >= 0) nq = std::max(nq, h.seg_bone_off[sg + 1] - h.seg_bone_off[sg]);
 		}
-		rows[i] = make_int4(h.sched[i].seg, h.sched[i].j, h.sched[i].m, h.sched[i].xs | (nq << 8));
+		rows[i] = make_int4(h.sched[i].seg, h.sched[i].j, h.sched[i].m, h.sched[i].flags | (nq << 8));
 	}
 	add(rows.data(), rows.size() * sizeof(int4), 4, d.o_sched);
 #define MBIK_ADD(T, name) \
@@ -2209,16 +2144,36 @@ bool helper_on(const mbik_plan *p) {
 	return lds <= 160 * 1024;
 }
 
-// After a synchronized helper-wave launch: a wave that gave up waiting (help_wait's exit, a
-// protocol error) leaves its count in g_mbik_help_stuck; report it instead of returning
-// results computed from unfinished records.
-int helper_stuck_check() {
-	unsigned int n = 0;
-	if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_mbik_help_stuck), sizeof(n)) != hipSuccess) return fail(MBIK_EHIP, "hipMemcpyFromSymbol");
-	if (n == 0) return MBIK_OK;
-	const unsigned int z = 0;
-	(void)hipMemcpyToSymbol(HIP_SYMBOL(g_mbik_help_stuck), &z, sizeof(z));
-	return fail(MBIK_EHIP, "helper wave: a wave timed out waiting for its partner (" + std::to_string(n) + " waves); results invalid");
+// The helper wave's handshake deadline: a wait gives up when the awaited counter has not moved
+// for this long.  A real wait lasts at most one iteration of the partner wave (under a
+// millisecond at the BASELINE sizes, tens of milliseconds for a 4,096-bone chain).
+constexpr int kHelpTimeoutMs = 2000;
+// A helper-wave launch needs the plan's timeout flag and the deadline in wall-clock ticks.
+int ensure_help_flag(mbik_plan *p) {
+	if (!p->help_flag) {
+		void *h = nullptr;
+		if (hipHostMalloc(&h, sizeof(unsigned int), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+			return fail(MBIK_ENOMEM, "hipHostMalloc helper timeout flag");
+		p->help_flag = static_cast<unsigned int *>(h);
+		*p->help_flag = 0u;
+		void *d = nullptr;
+		if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) return fail(MBIK_EHIP, "hipHostGetDevicePointer");
+		p->dev.help_flag = static_cast<unsigned int *>(d);
+	}
+	int khz = 0;
+	if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, p->device) != hipSuccess || khz <= 0) khz = 100000;
+	const uint64_t us = p->help_timeout_us > 0 ? (uint64_t)p->help_timeout_us : (uint64_t)kHelpTimeoutMs * 1000u;
+	p->dev.help_timeout = (uint64_t)khz * us / 1000u;
+	return MBIK_OK;
+}
+// Reports (once) a helper-wave timeout of an earlier launch of this plan: its skeletons were
+// written as failures (write_help_timeout) and flagged non-finite.  The asynchronous calls report
+// it on the plan's next call; the synchronous ones right after their own launch.
+int take_helper_timeout(mbik_plan *p) {
+	if (!p->help_flag || __atomic_load_n(p->help_flag, __ATOMIC_ACQUIRE) == 0u) return MBIK_OK;
+	__atomic_store_n(p->help_flag, 0u, __ATOMIC_RELEASE);
+	return fail(MBIK_EHIP, "helper wave: a launch of this plan timed out in the two-wave handshake; its skeletons "
+						   "were written as failures (identity rotation, NaN position) and flagged non-finite");
 }
 
 // Resident one-wave blocks per CU for a block's LDS size, from the runtime's occupancy
@@ -2330,23 +2285,31 @@ static size_t cmode_wave_words(const mbik_plan *p, int spw) {
 	const mbik::HostPlan &h = p->host;
 	return (size_t)spw * 4 * p->cm.W + 64 * ((size_t)p->cm.maxd + (h.stabilization_passes > 0 ? 3 * (size_t)h.P : 0));
 }
-size_t cmode_lds_bytes(const mbik_plan *p) {
-	const mbik::HostPlan &h = p->host;
-	return ((size_t)p->dev.topo_words + 2 * (size_t)h.B + (size_t)p->cm.wpb * cmode_wave_words(p, p->cm.spw)) * sizeof(float);
-}
 // constraint_mode launch shape: spw skeletons per wave (cm_spw_div halves 64 / K that many
 // times), and as many waves per block (<= kCmodeMaxWaves) as share the block's LDS within
 // 160 KiB and leave the launch with at least one block per CU.
-void cmode_shape(mbik_plan *p, int count) {
+struct CmShape {
+	int spw, wpb;
+};
+CmShape cmode_shape_of(const mbik_plan *p, int64_t count) {
 	const mbik::HostPlan &h = p->host;
 	const int full = 64 >> h.log2K;
-	p->cm.spw = p->spw_override > 0 ? std::min(full, p->spw_override) : std::max(1, full >> std::max(0, p->cm_spw_div));
+	const int spw = p->spw_override > 0 ? std::min(full, p->spw_override) : std::max(1, full >> std::max(0, p->cm_spw_div));
 	int wpb = kCmodeMaxWaves;
 	const size_t fixed = (size_t)p->dev.topo_words + 2 * (size_t)h.B;
-	while (wpb > 1 && ((fixed + (size_t)wpb * cmode_wave_words(p, p->cm.spw)) * sizeof(float) > 160 * 1024 ||
-							  (size_t)(count + (size_t)wpb * p->cm.spw - 1) / ((size_t)wpb * p->cm.spw) < (size_t)p->cu_count))
+	while (wpb > 1 && ((fixed + (size_t)wpb * cmode_wave_words(p, spw)) * sizeof(float) > 160 * 1024 ||
+							  (size_t)(count + (int64_t)wpb * spw - 1) / ((size_t)wpb * spw) < (size_t)p->cu_count))
 		wpb >>= 1;
-	p->cm.wpb = wpb;
+	return CmShape{spw, wpb};
+}
+size_t cmode_lds_bytes(const mbik_plan *p, CmShape sh) {
+	const mbik::HostPlan &h = p->host;
+	return ((size_t)p->dev.topo_words + 2 * (size_t)h.B + (size_t)sh.wpb * cmode_wave_words(p, sh.spw)) * sizeof(float);
+}
+void cmode_shape(mbik_plan *p, int count) {
+	const CmShape sh = cmode_shape_of(p, count);
+	p->cm.spw = sh.spw;
+	p->cm.wpb = sh.wpb;
 }
 
 // Resets the constraint_mode node caches of skeletons [first, first+count) to a fresh tree
@@ -2511,7 +2474,7 @@ int launch(mbik_plan *p, int first, int count, const float *pose_in, const float
 	if (rc) return rc;
 	if (h.constraint_mode) {
 		cmode_shape(p, count);
-		const size_t clds = cmode_lds_bytes(p);
+		const size_t clds = cmode_lds_bytes(p, CmShape{p->cm.spw, p->cm.wpb});
 		if (clds > 160 * 1024) return fail(MBIK_EUNSUPPORTED, "skeleton too large for the constraint_mode LDS layout");
 		static std::once_flag conce;
 		std::call_once(conce, [] {
@@ -2538,9 +2501,7 @@ int launch(mbik_plan *p, int first, int count, const float *pose_in, const float
 		return MBIK_OK;
 	}
 	size_t lds = ((size_t)h.spw * p->dev.lds_stride + p->dev.topo_words) * sizeof(float);
-#ifdef MBIK_ABLATE_SOALDS
-	lds += ((size_t)p->dev.B * 9 + p->dev.NC * p->dev.cf_stride + 2 * p->dev.NC * p->dev.cd_stride + 2) * sizeof(float);
-#endif
+	if constexpr (kAblate & ABL_SOALDS) lds += ((size_t)p->dev.B * 9 + p->dev.NC * p->dev.cf_stride + 2 * p->dev.NC * p->dev.cd_stride + 2) * sizeof(float);
 	if (lds > 160 * 1024) return fail(MBIK_EUNSUPPORTED, "skeleton too large for LDS at this lane count");
 	unsigned blocks = (unsigned)((count + h.spw - 1) / h.spw);
 	auto kern = solve_kernel_for(p);
@@ -2550,6 +2511,7 @@ int launch(mbik_plan *p, int first, int count, const float *pose_in, const float
 		std::call_once(honce, [] {
 			(void)hipFuncSetAttribute((const void *)mbik_solve_kernel_help, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 		});
+		if ((rc = ensure_help_flag(p)) != MBIK_OK) return rc;
 		kern = mbik_solve_kernel_help;
 		lds += kHelpRingBytes;
 		threads = 128;
@@ -3174,6 +3136,7 @@ void mbik_plan_destroy(mbik_plan *p) {
 	if (p->d_tg) (void)hipFree(p->d_tg);
 	if (p->d_out) (void)hipFree(p->d_out);
 	if (p->tile_ev) (void)hipEventDestroy(p->tile_ev);
+	if (p->help_flag) (void)hipHostFree(p->help_flag);
 	delete p;
 }
 
@@ -3195,7 +3158,8 @@ int32_t mbik_plan_get_info(const mbik_plan *p, mbik_plan_info *o) {
 	o->device_bytes = p->device_bytes;
 	o->algorithmic_bytes_per_skeleton = p->alg_bytes;
 	o->algorithmic_flops_per_skeleton = p->alg_flops;
-	o->lds_bytes_per_block = h.constraint_mode ? (int64_t)cmode_lds_bytes(p) : p->host.lds_block_bytes;
+	// (constraint_mode: the block of a whole-plan launch, independent of earlier launches' counts)
+	o->lds_bytes_per_block = h.constraint_mode ? (int64_t)cmode_lds_bytes(p, cmode_shape_of(p, h.N)) : p->host.lds_block_bytes;
 	o->checkpoint_interval = h.g_interval;
 	o->heading_staging = h.staging;
 	o->state_placement = h.state_hbm;
@@ -3435,7 +3399,7 @@ static int autotune_helper(mbik_plan *p, int first, int count, const float *pose
 	}
 	(void)hipEventDestroy(e0);
 	(void)hipEventDestroy(e1);
-	if (rc == MBIK_OK) rc = helper_stuck_check();
+	if (rc == MBIK_OK) rc = take_helper_timeout(p);
 	p->helper_override = rc == MBIK_OK && ms[1] * 1.015f < ms[0] ? 1 : 0;
 	return rc;
 }
@@ -3605,8 +3569,23 @@ int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const flo
 int32_t mbik_solve(mbik_plan *p, int32_t first, int32_t count, const float *pose_in, const float *targets, float *pose_out,
 		void *stream) {
 	if (!p) return fail(MBIK_EINVAL, "null plan");
+	if (int rc = take_helper_timeout(p)) return rc;
 	DeviceGuard guard(p->device);
 	return launch(p, first, count, pose_in, targets, pose_out, (hipStream_t)stream, p->host.iterations, 0, p->host.NS - 1);
+}
+
+int32_t mbik_plan_status(const mbik_plan *p, uint32_t *status) {
+	if (!p || !status) return fail(MBIK_EINVAL, "null argument");
+	*status = (p->help_flag && __atomic_load_n(p->help_flag, __ATOMIC_ACQUIRE)) ? MBIK_STATUS_HELPER_TIMEOUT : 0u;
+	return MBIK_OK;
+}
+
+int32_t mbik_plan_debug_helper(mbik_plan *p, int32_t drop_record, int32_t timeout_us) {
+	if (!p) return fail(MBIK_EINVAL, "null plan");
+	if (drop_record < -1 || timeout_us < 0) return fail(MBIK_EINVAL, "drop_record must be >= -1 and timeout_us >= 0");
+	p->dev.help_drop = drop_record;
+	p->help_timeout_us = timeout_us;
+	return MBIK_OK;
 }
 
 } // extern "C"
@@ -3846,6 +3825,7 @@ int32_t mbik_solve_checked(mbik_plan *p, int32_t first, int32_t count, const flo
 		float *pose_out, uint8_t *nonfinite, void *stream) {
 	if (!p) return fail(MBIK_EINVAL, "null plan");
 	if (!nonfinite) return fail(MBIK_EINVAL, "null nonfinite buffer");
+	if (int rc = take_helper_timeout(p)) return rc;
 	DeviceGuard guard(p->device);
 	if (p->host.P == 0 && count > 0 && first >= 0 && (int64_t)first + count <= p->host.N &&
 			hipMemsetAsync(nonfinite, 0, (size_t)count, (hipStream_t)stream) != hipSuccess)
@@ -3860,6 +3840,7 @@ int32_t mbik_segment_solve(mbik_plan *p, int32_t seg, int32_t first, int32_t cou
 		void *stream) {
 	if (!p) return fail(MBIK_EINVAL, "null plan");
 	if (seg < 0 || seg >= p->host.NS) return fail(MBIK_EINVAL, "segment out of range");
+	if (int rc = take_helper_timeout(p)) return rc;
 	DeviceGuard guard(p->device);
 	return launch(p, first, count, pose_inout, targets, pose_inout, (hipStream_t)stream, 1, p->host.seg_tin[seg], seg);
 }
@@ -3896,6 +3877,8 @@ int32_t mbik_group_solve(mbik_group *g, const int32_t *first, const int32_t *cou
 		const float *const *targets, float *const *pose_out, void *hip_stream) {
 	if (!g) return fail(MBIK_EINVAL, "null group");
 	if (!pose_in || !targets || !pose_out) return fail(MBIK_EINVAL, "null buffer array");
+	for (mbik_plan *p : g->plans)
+		if (int rc = take_helper_timeout(p)) return rc;
 	DeviceGuard guard(g->device);
 	hipStream_t stream = reinterpret_cast<hipStream_t>(hip_stream);
 	const int n = (int)g->plans.size();
@@ -4012,12 +3995,12 @@ int32_t mbik_solve_host(mbik_plan *p, int32_t first, int32_t count, const float 
 	if (hipMemcpy(p->d_in, pose_in, need * h.B * 10 * sizeof(float), hipMemcpyHostToDevice) != hipSuccess ||
 			(h.P > 0 && hipMemcpy(p->d_tg, targets, need * h.P * 12 * sizeof(float), hipMemcpyHostToDevice) != hipSuccess))
 		return fail(MBIK_EHIP, "hipMemcpy H2D");
+	if (int rc = take_helper_timeout(p)) return rc;
 	int rc = launch(p, first, count, p->d_in, p->d_tg, p->d_out, nullptr, h.iterations, 0, h.NS - 1);
 	if (rc) return rc;
-	const bool helped = helper_on(p);
 	if (hipMemcpy(pose_out, p->d_out, need * h.B * 10 * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess)
 		return fail(MBIK_EHIP, std::string("hipMemcpy D2H / kernel: ") + hipGetErrorString(hipGetLastError()));
-	return helped ? helper_stuck_check() : MBIK_OK;
+	return take_helper_timeout(p); // this launch's own (the copy waited for it)
 }
 
 } // extern "C"

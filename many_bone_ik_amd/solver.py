@@ -212,7 +212,9 @@ class Plan:
     def set_heading_staging(self, staging: int = -1):
         """mbik_plan_set_heading_staging: 1 stage multi-effector segments' headings in LDS,
         0 every lane solves such a segment alone, 2 stage only the translating root segments,
-        3 only segments with two or more effectors, -1 automatic; results do not depend on it."""
+        3 only segments with two or more effectors, 4 split-exchange (lanes build alternate
+        effectors' headings and read each other's cross-lane; two-waves-per-SIMD build only),
+        5 root segments as 2 and the rest as 4, -1 automatic; results do not depend on it."""
         check(self._L.mbik_plan_set_heading_staging(self.h, int(staging)))
 
     def set_locals_placement(self, placement: int = -1):
@@ -229,6 +231,18 @@ class Plan:
         parent-side work one step ahead (fully resident placement-0 launches), 0 off,
         -1 automatic."""
         check(self._L.mbik_plan_set_helper_wave(self.h, int(helper)))
+
+    def status(self) -> int:
+        """mbik_plan_status: MBIK_STATUS_HELPER_TIMEOUT (1) when a completed helper-wave launch of
+        this plan timed out in the two-wave handshake, else 0 (not cleared by reading)."""
+        st = C.c_uint32(0)
+        check(self._L.mbik_plan_status(self.h, C.byref(st)))
+        return int(st.value)
+
+    def debug_helper(self, drop_record: int = -1, timeout_us: int = 0):
+        """mbik_plan_debug_helper (test hook): the helper wave stops before record drop_record
+        (-1 never); the handshake deadline in microseconds (0 = the default two seconds)."""
+        check(self._L.mbik_plan_debug_helper(self.h, int(drop_record), int(timeout_us)))
 
     def set_table_addressing(self, wide: int = 0):
         """mbik_plan_set_table_addressing: 0 automatic (32-bit offsets below 4 GiB), 1 64-bit indices."""

@@ -9,6 +9,8 @@ Draw order per skeleton (fixed; changing it changes every fixture):
   1. for every bone b:   L ~ U[0.8, 1.2], axis ~ S^2 (2 draws), angle ~ U[0, 15 deg]
   2. for every bone b:   perturbation axis ~ S^2 (2 draws), angle ~ U[0, 30 deg]
   3. constrained configs, for every parented bone b: helper vector ~ S^2 (2 draws)
+  4. rest="realistic*" only, for every bone b: offset direction, roll, scale (7 draws,
+     ``_realistic_rest``)
 
 Pose layout  [skel][bone][10] = quaternion xyzw | position xyz | scale xyz  (float32)
 Target layout [skel][pin][12] = basis rows r0 r1 r2 | origin            (float32)
@@ -199,9 +201,51 @@ def custom_topology(parents, pins, constrained=(), cones_per_bone=0, twist=None,
                     np.asarray(constrained, np.int32), int(iterations), twist, int(cones_per_bone))
 
 
-def generate(cfg: int, n: int, first: int = 0, seed: int = SEED, topo: Topology | None = None) -> Workload:
+REST_MODES = ("plus_y", "realistic", "realistic_unit_scale")
+
+
+def _realistic_rest(rng: SplitMix64, n: int, B: int, length: np.ndarray, q_rest: np.ndarray):
+    """Draw order step 4 (the realistic modes only, after steps 1-3 so the default
+    stream is untouched), for every bone b:
+      offset direction: tilt ~ U[0, 110 deg] away from +Y, azimuth ~ U[0, 2pi)  (2 draws)
+      roll about the bone's own +Y ~ U[-180, 180 deg)                            (1 draw)
+      uniform scale ~ U[0.6, 1.6], then per-axis factors ~ U[0.8, 1.25]          (4 draws)
+    An imported humanoid's hips, clavicles and fingers sit off +Y, so
+    update_default_bone_direction_transform (ik_bone_3d.cpp:57-93) takes the general arc
+    branch; the rolls and non-uniform scales reach get_rotation_quaternion's
+    orthonormalization and get_scale (ik_bone_3d.cpp:170-179)."""
+    tilt = np.empty((n, B)); azim = np.empty((n, B)); roll = np.empty((n, B))
+    scale = np.empty((n, B, 3))
+    for b in range(B):
+        tilt[:, b] = math.radians(110.0) * rng.uniform()
+        azim[:, b] = 2.0 * math.pi * rng.uniform()
+        roll[:, b] = math.radians(360.0) * rng.uniform() - math.pi
+        s = 0.8 + 0.45 * rng.uniform()
+        for k in range(3):
+            scale[:, b, k] = s * (0.9 + 0.2 * rng.uniform())
+    direction = np.stack([np.sin(tilt) * np.cos(azim), np.cos(tilt), np.sin(tilt) * np.sin(azim)], -1)
+    pos = direction * length[..., None]
+    y_axis = np.broadcast_to(np.array([0.0, 1.0, 0.0]), (n, B, 3))
+    q = _quat_mul(q_rest, _quat_from_axis_angle(y_axis, roll))
+    return pos, q, scale
+
+
+def generate(cfg: int, n: int, first: int = 0, seed: int = SEED, topo: Topology | None = None,
+             rest: str = "plus_y") -> Workload:
     """Generate skeletons [first, first+n) of config ``cfg`` (1..5), or of ``topo`` (then
-    ``cfg`` only seeds the streams).  Constrained bones must not be parentless."""
+    ``cfg`` only seeds the streams).  Constrained bones must not be parentless.
+
+    ``rest="plus_y"`` (the default) puts every child at local (0, L, 0)
+    with unit scale.  ``rest="realistic"`` takes child offsets in random directions, bone
+    roll and non-uniform scale (``_realistic_rest``); the cones still centre on R_local*(+Y)
+    and the targets are the FK (scale included) of the perturbed pose.
+    ``rest="realistic_unit_scale"`` draws the same stream but keeps scale 1: on the long
+    constrained C5 rig any non-unit scale makes the reference's own solve overflow within
+    two iterations (the twist snap's P^-1 * orthonormalized(...) re-scales locals every step
+    and the translating root segment amplifies it; DESIGN.md §7 records the probe), so C5's
+    realistic fixture uses this mode."""
+    if rest not in REST_MODES:
+        raise ValueError(f"rest must be one of {REST_MODES}")
     topo = topology(cfg) if topo is None else topo
     B = topo.parents.shape[0]
     idx = np.arange(first, first + n, dtype=np.uint64)
@@ -219,14 +263,28 @@ def generate(cfg: int, n: int, first: int = 0, seed: int = SEED, topo: Topology 
     pos = np.zeros((n, B, 3))
     has_parent = topo.parents >= 0
     pos[:, has_parent, 1] = length[:, has_parent]
+    scale = np.ones((n, B, 3))
     pose = np.zeros((n, B, 10), np.float32)
+
+    C = topo.constrained.shape[0]
+    helper = np.zeros((n, B, 3))
+    if C:
+        for b in range(B):
+            if topo.parents[b] >= 0:
+                helper[:, b] = rng.unit_vector()
+    rest_dir = _quat_to_mat(q_rest)[..., :, 1]          # R_local * (0,1,0), parent frame (roll keeps it)
+    if rest != "plus_y":
+        r_pos, q_rest, r_scale = _realistic_rest(rng, n, B, length, q_rest)
+        pos[:, has_parent] = r_pos[:, has_parent]
+        if rest == "realistic":
+            scale = r_scale
     pose[..., 0:4] = q_rest
     pose[..., 4:7] = pos
-    pose[..., 7:10] = 1.0
+    pose[..., 7:10] = scale
 
     # Targets: FK of the perturbed pose; each pinned bone's global transform.
     q_pert = _quat_mul(_quat_from_axis_angle(pert_axis, pert_angle), q_rest)
-    R = _quat_to_mat(q_pert)
+    R = _quat_to_mat(q_pert) * scale[..., None, :]       # Basis(quat, scale): columns scaled
     G_R = np.empty((n, B, 3, 3)); G_o = np.empty((n, B, 3))
     order, seen = [], set()
 
@@ -257,11 +315,6 @@ def generate(cfg: int, n: int, first: int = 0, seed: int = SEED, topo: Topology 
     cones = np.zeros((n, C, mc, 4), np.float32)
     twist = np.zeros((n, C, 2), np.float32)
     if C:
-        helper = np.zeros((n, B, 3))
-        for b in range(B):
-            if topo.parents[b] >= 0:
-                helper[:, b] = rng.unit_vector()
-        rest_dir = _quat_to_mat(q_rest)[..., :, 1]          # R_local * (0,1,0), parent frame
         cb = topo.constrained
         c0 = rest_dir[:, cb]
         perp = np.cross(c0, helper[:, cb])
@@ -280,3 +333,31 @@ def generate(cfg: int, n: int, first: int = 0, seed: int = SEED, topo: Topology 
 
 def bench_config_name(cfg: int) -> str:
     return topology(cfg).name
+
+
+# SURVEY.md §8's serial critical path per iteration on Appendix C's spine topologies
+SURVEY_CRITICAL_PATH = {1: 8, 2: 11, 3: 11, 4: 16, 5: 30}
+
+
+def critical_path_steps(topo: Topology) -> int:
+    """Bone-steps per iteration on the longest root->leaf path of the IK bone list: the serial
+    chain one iteration costs when sibling segments run concurrently (the post-order recursion
+    of ik_bone_segment_3d.cpp:210-225 orders a segment after its children only).  Bones with no
+    pinned descendant are not solved (ik_bone_segment_3d.cpp:390-393) and do not count."""
+    B = topo.parents.shape[0]
+    pinned = np.zeros(B, bool)
+    for p in topo.pins:
+        b = int(p)
+        while b >= 0 and not pinned[b]:
+            pinned[b] = True                 # bone b has a pinned descendant (or is pinned)
+            b = int(topo.parents[b])
+    best = 0
+    for b in range(B):
+        if not pinned[b]:
+            continue
+        d, a = 0, b
+        while a >= 0:
+            d += 1
+            a = int(topo.parents[a])
+        best = max(best, d)
+    return best

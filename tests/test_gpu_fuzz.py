@@ -16,7 +16,7 @@ pytestmark = pytest.mark.gpu
 N_CASES = 48
 
 
-def random_case(seed: int):
+def random_case(seed: int, rest: str = "plus_y"):
     rng = np.random.default_rng(1000 + seed)
     B = int(rng.integers(2, 40))
     n_roots = 1 if rng.random() < 0.7 else int(rng.integers(2, 4))
@@ -37,7 +37,7 @@ def random_case(seed: int):
     twist = (float(rng.uniform(-math.pi, math.pi)), float(rng.uniform(0.05, 2 * math.pi)))
     topo = W.custom_topology(parents, pins, constrained, cones_per_bone=cones_per_bone, twist=twist,
                              iterations=int(rng.integers(1, 13)), name=f"fuzz{seed}")
-    wl = W.generate(9, 6, first=seed * 7, topo=topo)
+    wl = W.generate(9, 6, first=seed * 7, topo=topo, rest=rest)
     P, C = len(pins), len(constrained)
     wl.pin_weight = rng.choice([0.0, 0.3, 1.0, 2.5], P).astype(np.float32)
     wl.pin_weight[int(rng.integers(0, P))] = 1.0          # at least one weighted pin

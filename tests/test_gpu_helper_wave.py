@@ -12,7 +12,7 @@ from many_bone_ik_amd.solver import Plan
 from .test_gpu_parity import assert_parity
 
 pytestmark = pytest.mark.gpu
-RING_BYTES = 4 * 18 * 64 * 16 + 16   # solve.hip: kHelpRingBytes (kHelpSlots x kHelpF4 float4 per lane + counters)
+RING_BYTES = 4 * 18 * 64 * 16 + 32   # solve.hip: kHelpRingBytes (kHelpSlots x kHelpF4 float4 per lane + counters)
 
 
 def _helper_fits(info):
@@ -148,3 +148,68 @@ def test_helper_wave_argument_check(mbik):
             plan.set_helper_wave(bad)
         assert e.value.code == _lib.MBIK_EINVAL
     plan.set_helper_wave(-1)
+
+
+def _timeout_marker_ok(out, ref_shape_bones_in_list=None):
+    """write_help_timeout: identity rotation, NaN position, unit scale for every solved bone."""
+    q, o, sc = out[..., 0:4], out[..., 4:7], out[..., 7:10]
+    return (np.all(q == np.array([0, 0, 0, 1], np.float32)) and np.isnan(o).all() and np.all(sc == 1.0))
+
+
+def test_helper_timeout_is_visible_per_plan(oracle, mbik):
+    """VERDICT r3 item 3 / ADVICE r3: a helper wave that stops producing records (test hook:
+    mbik_plan_debug_helper drops record 5, 20 ms deadline) makes its partner give up; every
+    skeleton of the launch is written as a failure and flagged by mbik_solve_checked, the plan's
+    status shows the timeout, its next asynchronous call returns MBIK_EHIP once, and a second plan
+    solving concurrently on another stream sees none of it and stays bitwise exact."""
+    torch, dev = _dev()
+    wl = W.generate(2, 256, first=25000)
+    ref = oracle.Oracle(wl).solve(wl.pose, wl.targets, threads=8)
+    a, b = Plan.from_workload(wl), Plan.from_workload(wl)
+    for p in (a, b):
+        p.set_helper_wave(1)
+    a.debug_helper(5, 20000)
+    pi = torch.from_numpy(wl.pose).to(dev)
+    tg = torch.from_numpy(wl.targets).to(dev)
+    oa, ob = torch.empty_like(pi), torch.empty_like(pi)
+    fa = torch.zeros(wl.n, dtype=torch.uint8, device=dev)
+    fb = torch.ones(wl.n, dtype=torch.uint8, device=dev)
+    sa, sb = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    torch.cuda.synchronize()
+    a.solve_checked(pi.data_ptr(), tg.data_ptr(), oa.data_ptr(), fa.data_ptr(), stream=sa.cuda_stream)
+    b.solve_checked(pi.data_ptr(), tg.data_ptr(), ob.data_ptr(), fb.data_ptr(), stream=sb.cuda_stream)
+    torch.cuda.synchronize()
+    assert a.info()["helper_wave"] == 1 and b.info()["helper_wave"] == 1
+    assert a.status() == 1 and b.status() == 0
+    got_a = oa.cpu().numpy()
+    assert fa.cpu().numpy().all(), "a timed-out launch must flag every skeleton"
+    assert _timeout_marker_ok(got_a)
+    assert not fb.cpu().numpy().any()
+    assert_parity(ob.cpu().numpy(), ref, "concurrent plan on another stream")
+    # the next asynchronous call reports it (once, without launching), then the plan works again
+    with pytest.raises(_lib.MbikError) as e:
+        a.solve(pi.data_ptr(), tg.data_ptr(), oa.data_ptr())
+    assert e.value.code == _lib.MBIK_EHIP and "timed out" in str(e.value)
+    assert a.status() == 0
+    a.debug_helper(-1, 0)
+    a.solve(pi.data_ptr(), tg.data_ptr(), oa.data_ptr())
+    torch.cuda.synchronize()
+    assert a.status() == 0
+    assert_parity(oa.cpu().numpy(), ref, "the plan after its timeout was reported")
+    # the synchronous call reports its own launch's timeout
+    a.debug_helper(0, 20000)
+    with pytest.raises(_lib.MbikError) as e:
+        a.solve_host(wl.pose, wl.targets)
+    assert e.value.code == _lib.MBIK_EHIP
+    assert a.status() == 0 and b.status() == 0
+    a.debug_helper(-1, 0)
+    assert_parity(a.solve_host(wl.pose, wl.targets), ref, "solve_host after the timeout")
+
+
+def test_helper_debug_hook_argument_check(mbik):
+    plan = Plan.from_workload(W.generate(3, 2))
+    for args in ((-2, 0), (0, -1)):
+        with pytest.raises(_lib.MbikError) as e:
+            plan.debug_helper(*args)
+        assert e.value.code == _lib.MBIK_EINVAL
+    assert plan.status() == 0

@@ -295,12 +295,14 @@ def test_waves_argument_check(mbik):
 
 
 @pytest.mark.parametrize("cfg,n,pin", [(3, 65536, None), (5, 16384, (8, 8, 2, 4, 2, 2)), (5, 16384, (8, 8, 1, 0, 2, 2)),
+                                       (5, 16384, (8, 8, 1, 4, 2, 2)),
                                        (4, 32768, None), (4, 262144, (4, 16, 1, 4, 2, 2))])
 def test_tuned_full_size_layouts_are_exact(oracle, mbik, cfg, n, pin):
     """Full-size launches on the layouts autotune picks for them (C3, and C4 at its 32,768
     skeletons per GPU: autotuned here; C5: the layout its autotune picks, pinned -- 8 lanes x 8,
     checkpoint every 2nd bone, split-exchange headings (staging 4), all state in device memory,
-    two waves per SIMD -- and round 2's unstaged one; C4's whole 262,144-skeleton batch
+    two waves per SIMD -- the same with a checkpoint at every bone (the layout round 3's C5
+    bench line ran, K8_s8_i1_st4_pl2_w2), and round 2's unstaged one; C4's whole 262,144-skeleton batch
     of BASELINE configs[3] on one GPU: the strong-scaling layout, pinned -- 4 lanes x 16,
     split-exchange, all state in device memory (each area < 4 GiB: the buffer-resource guard),
     two waves per SIMD); oracle

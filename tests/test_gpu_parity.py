@@ -44,8 +44,9 @@ def test_configs_bitwise_vs_oracle(oracle, mbik, cfg, n, lanes):
 @pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "oracle_c*.npz"))),
                          ids=os.path.basename)
 def test_golden_fixtures(mbik, path):
+    from tests.golden.make_golden import generate
     f = np.load(path, allow_pickle=False)
-    wl = W.generate(int(f["cfg"]), int(f["n"]), first=int(f["first"]))
+    wl = generate(f)
     plan = Plan.from_workload(wl)
     assert_parity(plan.solve_host(wl.pose, wl.targets), f["pose_out"], os.path.basename(path))
     r, t, _ = plan.segment_table()

@@ -6,7 +6,6 @@ import os
 import numpy as np
 import pytest
 
-from many_bone_ik_amd import workloads as W
 
 FIX = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "oracle_c*.npz")))
 
@@ -18,16 +17,17 @@ def load(path):
 
 @pytest.mark.parametrize("path", FIX, ids=os.path.basename)
 def test_generator_digest_stable(path):
-    from tests.golden.make_golden import input_digest
+    from tests.golden.make_golden import generate, input_digest
     f = load(path)
-    wl = W.generate(int(f["cfg"]), int(f["n"]), first=int(f["first"]))
+    wl = generate(f)
     assert input_digest(wl) == str(f["digest"])
 
 
 @pytest.mark.parametrize("path", FIX, ids=os.path.basename)
 def test_oracle_reproduces_fixture(oracle, path):
+    from tests.golden.make_golden import generate
     f = load(path)
-    wl = W.generate(int(f["cfg"]), int(f["n"]), first=int(f["first"]))
+    wl = generate(f)
     o = oracle.Oracle(wl)
     out, trace = o.solve(wl.pose, wl.targets, trace=True)
     assert np.array_equal(out.view(np.uint32), f["pose_out"].view(np.uint32))
