@@ -40,7 +40,7 @@ def main():
     rec = {"fetch_size_kb": fk, "write_size_kb": wk, "dispatches": [nf, nw],
            "read_bytes": fk * 1024 * 2, "write_bytes": wk * 1024,
            "hbm_bytes_per_launch": fk * 1024 * 2 + wk * 1024,
-           "correction": "FETCH_SIZE x2 (gfx950, guide HBM section; uncalibrated for dword loads), KB x1024"}
+           "correction": "FETCH_SIZE x2 (gfx950, guide HBM section; calibrated for this kernel's b32/b64/b128, tiled and gathered buffer loads in round 3: profiles/r03_fetch_calib.json), KB x1024"}
     tj = json.load(open(out)) if os.path.exists(out) else {}
     tj[key] = rec
     with open(out, "w") as f:
