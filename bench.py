@@ -280,7 +280,20 @@ def main():
     if os.path.exists(args.valu_mix_json):
         try:
             vm = json.load(open(args.valu_mix_json)).get(tkey)  # the mix of exactly this layout
-            if vm:
+            if vm and "solver_issue_frac" in vm:
+                # helper-wave layout: the solving wave's own instructions (replay launch) over its
+                # cycles; the helper's share beside it (tools/replay_count.sh, tools/solver_issue.py)
+                issue = {"bound": "valu_issue_1wave", "wave": "solving",
+                         "achieved_cycles_per_wave": vm["solver_valu_issue_floor_cycles"],
+                         "valu_insts_per_wave": vm["solver_valu_insts_per_wave"],
+                         "wave_cycles": vm["solver_wave_cycles"], "frac": vm["solver_issue_frac"],
+                         "helper_valu_insts_per_wave": vm["helper_valu_insts_per_wave"],
+                         "helper_frac": vm["helper_issue_frac"],
+                         "note": "4 cycles per wave64 VALU instruction x the SOLVING wave's VALU instructions (counted on "
+                                 "a replay launch of that wave alone, bitwise-equal output) / its wave cycles in the "
+                                 "helper-wave launch (PMC, profiles/valu_mix.json); the ceiling this latency-bound "
+                                 "chain runs against"}
+            elif vm:
                 issue = {"bound": "valu_issue_1wave", "achieved_cycles_per_wave": vm["valu_issue_floor_cycles"],
                          "wave_cycles": vm["wave_cycles"], "frac": vm["issue_frac"],
                          "note": "4 cycles per wave64 VALU instruction x VALU instructions / wave cycles (PMC, "

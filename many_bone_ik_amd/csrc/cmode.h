@@ -236,8 +236,16 @@ struct CmodeLane {
 // headings' origins for stabilization), the swing snap (ik_kusudama_3d.cpp:347-376), the
 // twist snap (:117-132) and, for stabilized root segments, the MSD accept / restore loop
 // (ik_bone_segment_3d.cpp:163-180).  OE: the lane's target-heading origins, OE[64 * (3e + i)].
+// j / m: this lane's index in the segment's lane group and the group's size.  Every lane of the
+// group runs the step (the same reads, products and stores of the same bits); the heading
+// builds' node reads are split over the group: lane j reads effectors e0+j, e0+j+m, ...  Those
+// reads only fill caches -- a dirty node is recomputed top-down from its first clean ancestor,
+// nothing they touch changes a local -- so which lane fills a node, and in which order, leaves
+// the same cached bits and dirty words as the reference's sequential loop; lanes that share a
+// chain recompute it alike.  Stabilized segments keep every read on every lane: the MSD loop
+// needs each effector's target-heading origin on the lane that sums them.
 template <bool STAB, bool NB32>
-__device__ void cmode_step(const CmodeLane<NB32> &C, int seg, int k, const float *tg, float *OE, double &prev_dev) {
+__device__ void cmode_step(const CmodeLane<NB32> &C, int seg, int k, int j, int m, const float *tg, float *OE, double &prev_dev) {
 	const int ls = 64;
 	const DevPlan &t = C.t;
 	const int b = t.seg_bones[k];
@@ -248,7 +256,8 @@ __device__ void cmode_step(const CmodeLane<NB32> &C, int seg, int k, const float
 	uint64_t *pf = C.pf;
 #endif
 	MBIK_PROF_T(c0);
-	for (int i = e0; i < e1; i++) {
+	const int i0 = stab ? e0 : e0 + j, di = stab ? 1 : m;
+	for (int i = i0; i < e1; i += di) {
 		const int e = t.seg_effs[i];
 		if (stab) {
 			const X3 E = C.bdir_global(t.eff_bone[e]);
@@ -430,13 +439,13 @@ __global__ __launch_bounds__(64 * kCmodeMaxWaves) void mbik_cmode_kernel(DevPlan
 		if constexpr (!CHAIN) {
 		for (int r = 0; r < t.nrows; r++) {
 			const int4 task = t.sched[r * K + role];
-			if (valid && task.x >= seg_lo && task.x <= seg_hi && task.y == 0) {
+			if (valid && task.x >= seg_lo && task.x <= seg_hi) {
 				const int root = t.seg_bones[t.seg_bone_off[task.x + 1] - 1];
 				C.lo = pre[root];
 				C.hi = pre[root] + sub[root];
 				double prev_dev = INFINITY; // reset after the segment root bone (:178-180)
 				for (int k = t.seg_bone_off[task.x]; k < t.seg_bone_off[task.x + 1]; k++)
-					cmode_step<STAB, NB32>(C, task.x, k, tg, OE, prev_dev);
+					cmode_step<STAB, NB32>(C, task.x, k, task.y, task.z, tg, OE, prev_dev);
 			}
 			__syncthreads();
 			// The cleaning the reference's first read above the segment root did: the dirty
@@ -467,13 +476,13 @@ __global__ __launch_bounds__(64 * kCmodeMaxWaves) void mbik_cmode_kernel(DevPlan
 			// pending chain is kept (p0..p3) and cleaned after the level.
 			int r1 = r + 1;
 			while (r1 < t.nrows && (t.sched[r1 * K].w & mbik::SCHED_CHAIN)) r1++;
-			int rr = r - 1, k = 0, ke = 0, seg = 0;
+			int rr = r - 1, k = 0, ke = 0, seg = 0, j = 0, m = 1;
 			int p1 = -1, p2 = -1, p3 = -1;
 			double prev_dev = INFINITY;
 			for (;;) {
 				while (k >= ke && rr + 1 < r1) {
 					const int4 task = t.sched[++rr * K + role];
-					if (valid && task.x >= seg_lo && task.x <= seg_hi && task.y == 0) {
+					if (valid && task.x >= seg_lo && task.x <= seg_hi) {
 						if (pend >= 0) {
 							p3 = p2;
 							p2 = p1;
@@ -481,6 +490,8 @@ __global__ __launch_bounds__(64 * kCmodeMaxWaves) void mbik_cmode_kernel(DevPlan
 							pend = -1;
 						}
 						seg = task.x;
+						j = task.y;
+						m = task.z;
 						const int root = t.seg_bones[t.seg_bone_off[seg + 1] - 1];
 						C.lo = pre[root];
 						C.hi = pre[root] + sub[root];
@@ -490,13 +501,13 @@ __global__ __launch_bounds__(64 * kCmodeMaxWaves) void mbik_cmode_kernel(DevPlan
 					}
 				}
 				if (k >= ke) break;
-				cmode_step<STAB, NB32>(C, seg, k, tg, OE, prev_dev);
+				cmode_step<STAB, NB32>(C, seg, k, j, m, tg, OE, prev_dev);
 				k++;
 			}
 			__syncthreads();
 			// The cleaning the reference's first read above the segment root did: the dirty
 			// chain from the recorded node up, one lane at a time (siblings share it).
-			MBIK_PROF_T(r0);
+			MBIK_PROF_T(rc0);
 #pragma unroll
 			for (int q = 0; q < 4; q++) {
 				uint64_t todo = __ballot(pend >= 0);
@@ -516,8 +527,8 @@ __global__ __launch_bounds__(64 * kCmodeMaxWaves) void mbik_cmode_kernel(DevPlan
 				p3 = -1;
 				if (!__any(pend >= 0)) break;
 			}
-			MBIK_PROF_T(r1);
-			MBIK_PROF_ADD(8, r0, r1);
+			MBIK_PROF_T(rc1);
+			MBIK_PROF_ADD(8, rc0, rc1);
 			__syncthreads();
 			r = r1;
 		}

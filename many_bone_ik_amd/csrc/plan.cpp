@@ -689,16 +689,27 @@ void build_schedule(HostPlan &p, int32_t lanes, int64_t nlaunch, int32_t spw_ove
 			p.nrows++;
 		}
 	}
-	// Staged-heading LDS area (solve.hip, segments solved by several lanes of a row): 12
-	// floats per heading plus 24 for the exchanged sums.  The segments of one row run
-	// concurrently, so their areas are disjoint; offsets restart at every row.
+	// Staged-heading area (solve.hip, segments solved by several lanes of a row): 12 floats per
+	// heading plus 24 for the exchanged sums.  A translating split-exchange segment (staging 4 /
+	// 5, state placement 2) keeps there instead the effector globals its lanes built in the centroid pass, 12
+	// floats per lane and round, so that the sums pass rebuilds their headings without walking
+	// the paths again.  The segments of one row run concurrently, so their areas are disjoint;
+	// offsets restart at every row.
 	p.seg_hbase.assign(p.NS, 0);
 	p.hs_floats = 0;
 	for (int r = 0; r < p.nrows; r++) {
 		int used = 0;
 		for (int l = 0; l < K; l++) {
 			const SchedTask &tk = p.sched[(size_t)r * K + l];
-			if (tk.seg < 0 || tk.j != 0 || tk.m < 2 || (tk.flags & SCHED_XS) || p.seg_nh[tk.seg] < 2) continue;
+			if (tk.seg < 0 || tk.j != 0 || tk.m < 2 || p.seg_nh[tk.seg] < 2) continue;
+			if (tk.flags & SCHED_XS) {
+				// (only with the whole state in device memory: in LDS the area would cost residency)
+				if (!(p.seg_flags[tk.seg] & SF_TRANSLATE) || p.state_hbm != 2) continue;
+				const int ne = p.seg_eff_off[tk.seg + 1] - p.seg_eff_off[tk.seg];
+				p.seg_hbase[tk.seg] = used;
+				used += 12 * tk.m * ((ne + tk.m - 1) / tk.m);
+				continue;
+			}
 			p.seg_hbase[tk.seg] = used;
 			used += 12 * p.seg_nh[tk.seg] + 24;
 		}

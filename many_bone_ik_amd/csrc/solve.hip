@@ -112,6 +112,14 @@ struct DevPlan {
 	unsigned int *help_flag = nullptr;
 	uint64_t help_timeout = 0;
 	int help_drop = -1;
+#ifdef MBIK_REPLAY
+	// Diagnostic build (tools/replay_count.sh): the helper wave's records of one launch saved to
+	// rec_dump ([block][record][kHelpF4][64 lanes] float4), and a launch of the solving wave alone
+	// that reads them back instead of waiting for a helper -- its instruction counters are then
+	// the solving wave's own.  replay: 0 off, 1 save, 2 replay.
+	float4 *rec_dump = nullptr;
+	int rec_per_block = 0, replay = 0;
+#endif
 };
 
 // ------------------------------------------------------------------------------------
@@ -259,7 +267,10 @@ __device__ __forceinline__ void st_x(BPtr<float> p, const X3 &t) {
 // LocContig (BS 12, QS 4) is one skeleton's [B][12] block (LDS, or the whole state in device
 // memory); LocTiled interleaves the quads of kLocTile consecutive skeletons,
 // [N/kLocTile][B][3][kLocTile][4], so the lanes of one role in a wave (consecutive skeletons,
-// same bone) read whole cache lines.
+// same bone) read whole cache lines.  The quads hold the transform pair-aligned for the packed
+// arithmetic (gd_math.h GD_PACK: the x, y of a row go through one v_pk op from two adjacent
+// registers): [r0.x r0.y r1.x r1.y] [r2.x r2.y r0.z r1.z] [o.x o.y o.z r2.z], so every row's and
+// the origin's (x, y) pair lands even-aligned in the loaded registers and needs no moves.
 constexpr int kLocTile = 16;
 template <int BS, int QS, class PT>
 struct LocV {
@@ -270,17 +281,17 @@ struct LocV {
 		const float4 b = ld4(q + QS);
 		const float4 c = ld4(q + 2 * QS);
 		X3 t;
-		t.b.r[0] = v3(a.x, a.y, a.z);
-		t.b.r[1] = v3(a.w, b.x, b.y);
-		t.b.r[2] = v3(b.z, b.w, c.x);
-		t.o = v3(c.y, c.z, c.w);
+		t.b.r[0] = v3(a.x, a.y, b.z);
+		t.b.r[1] = v3(a.z, a.w, b.w);
+		t.b.r[2] = v3(b.x, b.y, c.w);
+		t.o = v3(c.x, c.y, c.z);
 		return t;
 	}
 	__device__ __forceinline__ void st(int i, const X3 &t) const {
 		const auto q = p + BS * i;
-		st4(q, make_float4(t.b.r[0].x, t.b.r[0].y, t.b.r[0].z, t.b.r[1].x));
-		st4(q + QS, make_float4(t.b.r[1].y, t.b.r[1].z, t.b.r[2].x, t.b.r[2].y));
-		st4(q + 2 * QS, make_float4(t.b.r[2].z, t.o.x, t.o.y, t.o.z));
+		st4(q, make_float4(t.b.r[0].x, t.b.r[0].y, t.b.r[1].x, t.b.r[1].y));
+		st4(q + QS, make_float4(t.b.r[2].x, t.b.r[2].y, t.b.r[0].z, t.b.r[1].z));
+		st4(q + 2 * QS, make_float4(t.o.x, t.o.y, t.o.z, t.b.r[2].z));
 	}
 };
 using LocContig = LocV<12, 4, float *>;
@@ -540,7 +551,8 @@ struct PathCk {
 };
 template <class LV, class FP, class IP>
 __device__ __forceinline__ void effector_headings(const DevPlan &t, const EffPre &p, int d0, const X3 &Gb, const LV &L,
-		const FP ST, const IP SF, Headings &H, const FP OE, int oe_mode = 0, PathCk *pc = nullptr, const int *lcp = nullptr) {
+		const FP ST, const IP SF, Headings &H, const FP OE, int oe_mode = 0, PathCk *pc = nullptr, const int *lcp = nullptr,
+		X3 *eout = nullptr) {
 	const int e = p.e;
 	X3 E;
 	if (SF[e]) {
@@ -551,16 +563,20 @@ __device__ __forceinline__ void effector_headings(const DevPlan &t, const EffPre
 		const int off = p.off;
 		const int de = p.de;
 		// X *= L(path[d]) for d = a..b, software-pipelined: the next path bone's local pose
-		// loads during the current product
+		// loads during the current product.  Two products per trip, so the two pose registers
+		// keep their roles (one trip per product rotated 12 registers each time: ~20 % of the
+		// loop's instructions were those moves); the last trip's look-ahead re-reads path[b].
 		auto walk = [&](int a, int b) {
 			if (a > b) return;
-			X3 Ln = L.ld(t.eff_path[off + a]);
-			for (int d = a; d < b; d++) {
-				const X3 Lc = Ln;
-				Ln = L.ld(t.eff_path[off + d + 1]);
-				X = X * Lc;
+			X3 L0 = L.ld(t.eff_path[off + a]);
+			int d = a;
+			for (; d < b; d += 2) {
+				const X3 L1 = L.ld(t.eff_path[off + d + 1]);
+				X = X * L0;
+				L0 = L.ld(t.eff_path[off + min(d + 2, b)]);
+				X = X * L1;
 			}
-			X = X * Ln;
+			if (d == b) X = X * L0;
 		};
 		int d = d0;
 		if (pc) {
@@ -589,6 +605,7 @@ __device__ __forceinline__ void effector_headings(const DevPlan &t, const EffPre
 		E.b = X.b * p.Db;
 		E.o = X.o;
 	}
+	if (eout) *eout = E;
 	V3 oe = E.o;         // target headings: the effector's own bone origin (:97)
 	if (oe_mode == 1) {
 		OE[3 * e] = oe.x; OE[3 * e + 1] = oe.y; OE[3 * e + 2] = oe.z;
@@ -600,10 +617,10 @@ __device__ __forceinline__ void effector_headings(const DevPlan &t, const EffPre
 template <int TA, class LV, class FP, class IP>
 __device__ __forceinline__ void effector_headings(const DevPlan &t, int e, int d0, const X3 &Gb, const LV &L,
 		const FP TG, const FP ST, const IP SF, size_t s, const double *hw, Headings &H, const FP OE,
-		int oe_mode = 0, PathCk *pc = nullptr, const int *lcp = nullptr) {
+		int oe_mode = 0, PathCk *pc = nullptr, const int *lcp = nullptr, X3 *eout = nullptr) {
 	EffPre p;
 	load_eff<TA>(t, e, TG, s, hw, p);
-	effector_headings(t, p, d0, Gb, L, ST, SF, H, OE, oe_mode, pc, lcp);
+	effector_headings(t, p, d0, Gb, L, ST, SF, H, OE, oe_mode, pc, lcp, eout);
 }
 
 // The heading pairs of effector p.e (ik_effector_3d.cpp:90-149): E = the effector bone's
@@ -1018,13 +1035,26 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, int xs
 		// consumes all of them in the reference's effector order, exactly as the one-lane
 		// branch below does, so every sum rounds the same.  No staging memory.
 		const int lb = (int)__lane_id() - j;
-		auto each = [&](auto &&use) __attribute__((always_inline)) {
+		// A translating segment builds every heading twice (centroids, then sums, as
+		// weighted_superpose needs both): the first pass keeps each of this lane's effector
+		// globals in the segment's staging area (build_schedule), the second rebuilds the
+		// headings from them -- the same heading_terms of the same E, without walking the paths
+		// again.  (State placement 2 only, where that area is device memory: build_schedule.)
+		constexpr bool kXE = std::is_same_v<FP, BPtr<float>>;
+		const int rounds = (e1 - e0 + m - 1) / m;
+		const auto xe = HS + t.seg_hbase[seg] + 12 * rounds * j;
+		auto each = [&](auto &&use, int pass) __attribute__((always_inline)) {
 			PathCk pc;
 			pc.d = -1;
-			for (int i0 = e0; i0 < e1; i0 += m) {
+			for (int i0 = e0, r = 0; i0 < e1; i0 += m, r++) {
 				const int i = i0 + j;
 				Headings Hm;
-				if (i < e1) {
+				if (i < e1 && pass == 2) {
+					EffPre p;
+					load_eff<TA>(t, t.seg_effs[i], TG, s, hw + t.seg_eff_hoff[i], p);
+					const X3 E = ld_x(xe + 12 * r);
+					heading_terms(p, E, E.o, Gb.o, Hm);
+				} else if (i < e1) {
 					int lc[2] = {0, 0};
 					if (i - m >= e0) {
 						lc[0] = t.seg_eff_lcp[i];
@@ -1034,8 +1064,10 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, int xs
 						lc[1] = t.seg_eff_lcp[i + 1];
 						for (int u = i + 2; u <= i + m; u++) lc[1] = min(lc[1], t.seg_eff_lcp[u]);
 					}
+					X3 E;
 					effector_headings<TA>(t, t.seg_effs[i], d0, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], Hm, OE, oe_mode,
-							PR ? &pc : nullptr, lc);
+							PR ? &pc : nullptr, lc, pass == 1 ? &E : nullptr);
+					if (pass == 1) st_x(xe + 12 * r, E);
 				}
 				for (int v = 0; v < m && i0 + v < e1; v++) {
 					Headings H; // (weights and mask only)
@@ -1059,7 +1091,8 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, int xs
 				mc = mc + hm * (float)w;
 				tc = tc + ht * (float)w;
 				wsum += w;
-			});
+			}, kXE ? 1 : 0);
+			wave_sync_lds(); // (this lane's own records: program order, made explicit for device memory)
 			if (wsum > 0) {
 				mc = divs(mc, (float)wsum);
 				tc = divs(tc, (float)wsum);
@@ -1083,7 +1116,7 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, int xs
 			S.zx += (double)(wc1.z * c2.x);
 			S.zy += (double)(wc1.z * c2.y);
 			S.zz += (double)(wc1.z * c2.z);
-		});
+		}, kXE && translate ? 2 : 0);
 		qrot = qcp_adjugate(S);
 	} else if (m == 1 || nh == 0) {
 		// Several headings (or none: a pinless root segment, whose sums stay zero), one lane or
@@ -1489,47 +1522,52 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, int xs
 #endif
 }
 
-// The same products for the helper wave, whose global pass is the solving wave's wait at each
-// iteration start: the next bone's index and local load before this bone's product and store.
+// Iteration-start globals of one segment, root -> tip (IKNode3D::get_global_transform), with
+// the next bone's index and local loaded before this bone's product and store (the helper
+// wave's global pass is the solving wave's wait at each iteration start).
 template <class LV, class GV>
 __device__ void global_pass_pipelined(const DevPlan &t, int seg, const LV &L, const GV &G) {
+	// two bones per trip, so the two local registers keep their roles (no 12-register rotation
+	// per product); each product's successor local loads during it
 	const int kb = t.seg_bone_off[seg], kt = t.seg_bone_off[seg + 1] - 1;
-	int b = t.seg_bones[kt];
+	const int b = t.seg_bones[kt];
 	const int pp = t.bone_pose_parent[b];
-	X3 Gprev = pp >= 0 ? G.ld(t.bone_gslot[pp]) : xid();
-	const bool top_origin = pp == mbik::POSE_PARENT_ORIGIN;
-	X3 Lb = L.ld(b);
-	int gs = t.bone_gslot[b];
-	for (int k = kt; k >= kb; k--) {
-		X3 Ln = Lb;
-		int gn = -1;
-		if (k > kb) {
-			const int bn = t.seg_bones[k - 1];
-			Ln = L.ld(bn);
-			gn = t.bone_gslot[bn];
+	X3 La = L.ld(b);
+	X3 Lb;
+	int ga = t.bone_gslot[b], gb = -1;
+	if (kt > kb) {
+		const int bn = t.seg_bones[kt - 1];
+		Lb = L.ld(bn);
+		gb = t.bone_gslot[bn];
+	}
+	X3 Gprev = pp >= 0 ? G.ld(t.bone_gslot[pp]) * La : (pp == mbik::POSE_PARENT_ORIGIN ? xid() * La : La);
+	if (ga >= 0) G.st(ga, Gprev);
+	int k = kt - 1;
+	for (; k > kb; k -= 2) { // bones k (in Lb) and k - 1
+		const int bn = t.seg_bones[k - 1];
+		La = L.ld(bn);
+		ga = t.bone_gslot[bn];
+		Gprev = Gprev * Lb;
+		if (gb >= 0) G.st(gb, Gprev);
+		if (k - 2 >= kb) {
+			const int bm = t.seg_bones[k - 2];
+			Lb = L.ld(bm);
+			gb = t.bone_gslot[bm];
 		}
-		const X3 Gb = k < kt ? Gprev * Lb : (pp >= 0 ? Gprev * Lb : (top_origin ? xid() * Lb : Lb));
-		if (gs >= 0) G.st(gs, Gb);
-		Gprev = Gb;
-		Lb = Ln;
-		gs = gn;
+		Gprev = Gprev * La;
+		if (ga >= 0) G.st(ga, Gprev);
+	}
+	if (k == kb) {
+		Gprev = Gprev * Lb;
+		if (gb >= 0) G.st(gb, Gprev);
 	}
 }
 
-// Iteration-start globals of one segment, root -> tip (IKNode3D::get_global_transform).
+// Iteration-start globals of one segment, root -> tip (IKNode3D::get_global_transform): the
+// pipelined pass above (its products and stores, in the same order).
 template <class LV, class GV>
-__device__ void global_pass(const DevPlan &t, int seg, const LV &L, const GV &G) {
-	X3 Gprev = xid();
-	for (int k = t.seg_bone_off[seg + 1] - 1; k >= t.seg_bone_off[seg]; k--) {
-		const int b = t.seg_bones[k];
-		const int pp = t.bone_pose_parent[b];
-		X3 Lb = L.ld(b);
-		X3 Gb;
-		if (k < t.seg_bone_off[seg + 1] - 1) Gb = Gprev * Lb; // parent = the bone just done
-		else Gb = pp >= 0 ? G.ld(t.bone_gslot[pp]) * Lb : (pp == mbik::POSE_PARENT_ORIGIN ? xid() * Lb : Lb);
-		if (t.bone_gslot[b] >= 0) G.st(t.bone_gslot[b], Gb);
-		Gprev = Gb;
-	}
+__device__ __forceinline__ void global_pass(const DevPlan &t, int seg, const LV &L, const GV &G) {
+	global_pass_pipelined(t, seg, L, G);
 }
 
 // IKBone3D::set_skeleton_bone_pose (ik_bone_3d.cpp:170-179); returns whether the basis was
@@ -1716,6 +1754,11 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 						}
 #endif
 						if (k0 + q < k1) help_part_b(t, k0 + q, P, Gbb, rw, rec);
+#ifdef MBIK_REPLAY
+						if (t.replay == 1)
+							for (int i = 0; i < kHelpF4; i++)
+								t.rec_dump[((size_t)blk * t.rec_per_block + seq) * kHelpF4 * 64 + (size_t)i * 64 + lane] = rec[i * 64];
+#endif
 						help_post(hfl + 1, seq + 1);
 						slot = slot + 1 == kHelpSlots ? 0 : slot + 1;
 					}
@@ -1729,6 +1772,11 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 		}
 		int seq = 0, slot = 0;
 		bool stuck = false;
+#ifdef MBIK_REPLAY
+		// replay: no partner to wait for (stuck skips every wait); records come from rec_dump
+		const float4 *rp = t.replay == 2 ? t.rec_dump + (size_t)blk * t.rec_per_block * kHelpF4 * 64 + lane : nullptr;
+		if (rp) stuck = true;
+#endif
 		for (int it = 0; it < iterations; it++) {
 			for (int r = 0; r < t.nrows; r++) {
 				const int4 task = t.sched[r * K + role];
@@ -1750,9 +1798,13 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 #ifdef MBIK_PROF
 					if (r == 0 && q == 0) MBIK_PROF_ADD(20, hw0, hw1);
 #endif
+					const float4 *hrec = ring + slot * (kHelpF4 * 64);
+#ifdef MBIK_REPLAY
+					if (rp) hrec = rp + (size_t)seq * kHelpF4 * 64;
+#endif
 					if (k0 + q < k1)
 						bone_step<false, true, kTab32, true, false>(t, seg, k0 + q, task.y, task.z, task.w & mbik::SCHED_XS, s, L, G, TG, ST, SF, HS, OE, MS, prev_dev,
-								pre, hoist, ring + slot * (kHelpF4 * 64), b_ready ? nullptr : hfl, seq, &stuck MBIK_PROF_ARG);
+								pre, hoist, hrec, b_ready ? nullptr : hfl, seq, &stuck MBIK_PROF_ARG);
 					help_post(hfl + 2, seq + 1);
 					slot = slot + 1 == kHelpSlots ? 0 : slot + 1;
 				}
@@ -1763,6 +1815,9 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 		// (the helper raises HC_STUCK before any record it writes without waiting, so a record
 		// this wave read from an overwritten slot is covered by the flag read here)
 		help_stuck = stuck || __builtin_amdgcn_readfirstlane(__hip_atomic_load(hfl + HC_STUCK, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) != 0;
+#ifdef MBIK_REPLAY
+		if (rp) help_stuck = false;
+#endif
 	} else
 	for (int it = 0; it < iterations; it++) {
 		MBIK_PROF_T(pg0);
@@ -1862,6 +1917,15 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 		int seg_hi) {
 	solve_block<false, 0, true, true, true>(t, xcd_block(), first, count, pose_in, targets, pose_out, iterations, seg_lo, seg_hi);
 }
+
+#ifdef MBIK_REPLAY
+// The solving wave alone, replaying saved helper records (diagnostic build only).
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void mbik_solve_kernel_replay(DevPlan t, int first, int count,
+		const float *__restrict__ pose_in, const float *__restrict__ targets, float *__restrict__ pose_out, int iterations, int seg_lo,
+		int seg_hi) {
+	solve_block<false, 0, true, true, true>(t, xcd_block(), first, count, pose_in, targets, pose_out, iterations, seg_lo, seg_hi);
+}
+#endif
 
 // A heterogeneous batch (mbik_group_solve): several plans -- distinct rigs -- in one launch.
 // Plan i owns blocks [block_off[i], block_off[i + 1]) of the grid; each block loads its
@@ -2515,6 +2579,16 @@ int launch(mbik_plan *p, int first, int count, const float *pose_in, const float
 		kern = mbik_solve_kernel_help;
 		lds += kHelpRingBytes;
 		threads = 128;
+#ifdef MBIK_REPLAY
+		if (p->dev.replay == 2) {
+			static std::once_flag ronce;
+			std::call_once(ronce, [] {
+				(void)hipFuncSetAttribute((const void *)mbik_solve_kernel_replay, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+			});
+			kern = mbik_solve_kernel_replay;
+			threads = 64;
+		}
+#endif
 	}
 	DevPlan d = p->dev;
 	if (h.state_hbm == 2) {
@@ -4004,6 +4078,45 @@ int32_t mbik_solve_host(mbik_plan *p, int32_t first, int32_t count, const float 
 }
 
 } // extern "C"
+
+#ifdef MBIK_REPLAY
+// Diagnostic: mode 1 runs a helper-wave solve that saves every helper record, mode 2 the solving
+// wave alone replaying them (same inputs, same skeletons), mode 0 frees the buffer.
+extern "C" int mbik_debug_replay(mbik_plan *p, int32_t mode, int32_t first, int32_t count, const float *pose_in,
+		const float *targets, float *pose_out, void *stream) {
+	DeviceGuard guard(p->device);
+	if (mode == 0) {
+		if (p->dev.rec_dump) (void)hipFree(p->dev.rec_dump);
+		p->dev.rec_dump = nullptr;
+		p->dev.replay = 0;
+		return MBIK_OK;
+	}
+	int rc = ensure_schedule(p, count);
+	if (rc) return rc;
+	if (!helper_on(p)) return fail(MBIK_EINVAL, "replay needs a helper-wave layout");
+	const mbik::HostPlan &h = p->host;
+	int per_iter = 0;
+	for (int r = 0; r < h.nrows; r++) {
+		int nq = 0;
+		for (int l = 0; l < h.K; l++) {
+			const int sg = h.sched[(size_t)r * h.K + l].seg;
+			if (sg >= 0) nq = std::max(nq, h.seg_bone_off[sg + 1] - h.seg_bone_off[sg]);
+		}
+		per_iter += nq;
+	}
+	const size_t blocks = (size_t)(count + h.spw - 1) / h.spw;
+	if (mode == 1) {
+		if (p->dev.rec_dump) (void)hipFree(p->dev.rec_dump);
+		p->dev.rec_per_block = per_iter * h.iterations;
+		if (hipMalloc(&p->dev.rec_dump, blocks * p->dev.rec_per_block * kHelpF4 * 64 * sizeof(float4)) != hipSuccess)
+			return fail(MBIK_ENOMEM, "replay buffer");
+	}
+	p->dev.replay = mode;
+	rc = launch(p, first, count, pose_in, targets, pose_out, (hipStream_t)stream, h.iterations, 0, h.NS - 1);
+	p->dev.replay = 0;
+	return rc;
+}
+#endif
 
 #ifdef MBIK_PROF
 extern "C" int mbik_debug_prof(unsigned long long *out) {
