@@ -50,7 +50,7 @@ extern "C" {
 #define MBIK_EUNSUPPORTED (-4)
 #define MBIK_ENODEV (-5)
 
-#define MBIK_ABI_VERSION 6
+#define MBIK_ABI_VERSION 7
 
 typedef struct mbik_plan mbik_plan;
 typedef struct mbik_group mbik_group;
@@ -113,6 +113,12 @@ typedef struct mbik_plan_info {
 	int32_t cd_stride;                 /* doubles per slot of CD = 2*max_cones (ABI 3) */
 	int32_t libm_variant;              /* mbik_plan_options.libm_variant the plan was created with (ABI 4) */
 	int32_t helper_wave;               /* 1 when the current layout launches with the helper wave (ABI 5) */
+	int32_t heading_slots;             /* 0x67 when every effector has the reference's default direction
+	                                      priorities (x, z > 0, y = 0: ik_effector_template_3d.h:45), so the
+	                                      plan launches the kernels built for that heading set; 0 when the
+	                                      priorities differ, and each effector's slots are tested at run
+	                                      time (ABI 7).  Bits: 0 the origin heading, 1+2a and 2+2a the
+	                                      +/- headings of axis a. */
 } mbik_plan_info;
 
 /* Which reference host the plan reproduces bit for bit (ABI 4).  Godot's Math::sin/cos(float)

@@ -69,7 +69,7 @@ class MbikPlanInfo(C.Structure):
                 ("checkpoint_interval", C.c_int32), ("heading_staging", C.c_int32), ("state_placement", C.c_int32),
                 ("waves_per_simd", C.c_int32), ("constraint_slots", C.c_int32), ("cf_stride", C.c_int32),
                 ("cd_stride", C.c_int32), ("libm_variant", C.c_int32),
-                ("helper_wave", C.c_int32)]
+                ("helper_wave", C.c_int32), ("heading_slots", C.c_int32)]
 
 
 class MbikPlanOptions(C.Structure):

@@ -78,6 +78,7 @@ struct DevPlan {
 	int B, P, NS, NC, max_cones, nrows, K, log2K, spw, lds_stride;
 	int N, cf_stride, cd_stride;
 	int stab;            // stabilization_passes (root segments only, SF_STAB)
+	int prio_mask = 0;   // kPrioDefault if every effector has that heading slot mask, else 0
 	int hs_floats;       // staged-heading LDS floats per skeleton
 	int n_gck;           // checkpoint globals per skeleton (HostPlan::bone_gslot)
 	int constraint_mode; // ManyBoneIK3D::constraint_mode
@@ -497,7 +498,19 @@ struct EffPre {
 	float pr[3];
 	double hws[7];
 };
-template <int TA, class FP>
+// Heading slot masks: bit 0 the origin heading, bits 1+2a / 2+2a the +/- headings of axis a
+// (present when direction priority a > 0).  PM != 0: every effector of the plan has that mask
+// (DevPlan::prio_mask), so the slot tests are compile-time constants and the heading loops
+// compile to straight-line code; PM == 0: tested per effector at run time.  The one
+// specialised mask is the reference's default priorities (0.2, 0, 0.2)
+// (ik_effector_template_3d.h:45): origin, +/-x, +/-z.
+constexpr int kPrioDefault = 1 | (6 << 0) | (6 << 4);
+template <int PM>
+__device__ __forceinline__ bool prio_on(float pr, int a) {
+	if constexpr (PM != 0) return ((PM >> (1 + 2 * a)) & 1) != 0;
+	else return pr > 0.0f;
+}
+template <int TA, int PM = 0, class FP>
 __device__ __forceinline__ void load_eff(const DevPlan &t, int e, const FP TG, size_t s, const double *hw, EffPre &p) {
 	p.e = e;
 	p.off = t.eff_path_off[e];
@@ -509,22 +522,24 @@ __device__ __forceinline__ void load_eff(const DevPlan &t, int e, const FP TG, s
 #pragma unroll
 	for (int a = 0; a < 3; a++) {
 		p.pr[a] = t.eff_prio[3 * e + a];
-		const bool on = p.pr[a] > 0.0f;
+		const bool on = prio_on<PM>(p.pr[a], a);
 		p.hws[1 + 2 * a] = on ? hw[k] : 0.0;
 		p.hws[2 + 2 * a] = on ? hw[k + 1] : 0.0;
 		k += on ? 2 : 0;
 	}
 }
+template <int PM = 0>
 __device__ __forceinline__ void heading_terms(const EffPre &p, const X3 &E, V3 oe, V3 ob, Headings &H);
 // The weights and slot mask heading_terms gives effector e's headings (from its priorities and
 // its QCP heading weights hw), without building the headings.
+template <int PM = 0>
 __device__ __forceinline__ void heading_weights(const DevPlan &t, int e, const double *hw, Headings &H) {
 	H.w[0] = hw[0];
 	H.mask = 1;
 	int k = 1;
 #pragma unroll
 	for (int a = 0; a < 3; a++) {
-		if (t.eff_prio[3 * e + a] > 0.0f) {
+		if (prio_on<PM>(t.eff_prio[3 * e + a], a)) {
 			H.w[1 + 2 * a] = hw[k];
 			H.w[2 + 2 * a] = hw[k + 1];
 			k += 2;
@@ -549,7 +564,7 @@ struct PathCk {
 	X3 x;
 	int d;
 };
-template <class LV, class FP, class IP>
+template <int PM, class LV, class FP, class IP>
 __device__ __forceinline__ void effector_headings(const DevPlan &t, const EffPre &p, int d0, const X3 &Gb, const LV &L,
 		const FP ST, const IP SF, Headings &H, const FP OE, int oe_mode = 0, PathCk *pc = nullptr, const int *lcp = nullptr,
 		X3 *eout = nullptr) {
@@ -612,20 +627,21 @@ __device__ __forceinline__ void effector_headings(const DevPlan &t, const EffPre
 	} else if (oe_mode == 2) {
 		oe = v3(OE[3 * e], OE[3 * e + 1], OE[3 * e + 2]);
 	}
-	heading_terms(p, E, oe, Gb.o, H);
+	heading_terms<PM>(p, E, oe, Gb.o, H);
 }
-template <int TA, class LV, class FP, class IP>
+template <int TA, int PM, class LV, class FP, class IP>
 __device__ __forceinline__ void effector_headings(const DevPlan &t, int e, int d0, const X3 &Gb, const LV &L,
 		const FP TG, const FP ST, const IP SF, size_t s, const double *hw, Headings &H, const FP OE,
 		int oe_mode = 0, PathCk *pc = nullptr, const int *lcp = nullptr, X3 *eout = nullptr) {
 	EffPre p;
-	load_eff<TA>(t, e, TG, s, hw, p);
-	effector_headings(t, p, d0, Gb, L, ST, SF, H, OE, oe_mode, pc, lcp, eout);
+	load_eff<TA, PM>(t, e, TG, s, hw, p);
+	effector_headings<PM>(t, p, d0, Gb, L, ST, SF, H, OE, oe_mode, pc, lcp, eout);
 }
 
 // The heading pairs of effector p.e (ik_effector_3d.cpp:90-149): E = the effector bone's
 // bone-direction global, T = its target, oe = the target headings' origin (E.o when built),
 // ob = the solved bone's bone-direction origin (:125).
+template <int PM>
 __device__ __forceinline__ void heading_terms(const EffPre &p, const X3 &E, V3 oe, V3 ob, Headings &H) {
 	const X3 &T = p.T;
 	H.ht[0] = T.o - oe;
@@ -637,7 +653,7 @@ __device__ __forceinline__ void heading_terms(const EffPre &p, const X3 &E, V3 o
 #pragma unroll
 	for (int a = 0; a < 3; a++) {
 		float pr = p.pr[a];
-		if (pr > 0.0f) {
+		if (prio_on<PM>(pr, a)) {
 			float w = (float)p.hws[1 + 2 * a];
 			H.w[1 + 2 * a] = p.hws[1 + 2 * a];
 			H.w[2 + 2 * a] = p.hws[2 + 2 * a];
@@ -942,11 +958,40 @@ __device__ __forceinline__ void help_part_b(const DevPlan &t, int k, const X3 &P
 constexpr int HS_REC = 12;
 template <class FP>
 __device__ __forceinline__ void qcp_terms(const V3 wc1, const V3 c1, const V3 c2, const FP r) {
-	r[0] = wc1.x * c2.x; r[1] = wc1.x * c2.y; r[2] = wc1.x * c2.z;
-	r[3] = wc1.y * c2.x; r[4] = wc1.y * c2.y; r[5] = wc1.y * c2.z;
-	r[6] = wc1.z * c2.x; r[7] = wc1.z * c2.y; r[8] = wc1.z * c2.z;
+	// the nine float products as four packed pairs and one scalar (each lane of a pair is the
+	// scalar IEEE product, so the terms are the same bits)
+#ifdef GD_PACK
+	const F2 px = xy(c2) * wc1.x, py = xy(c2) * wc1.y, pz = xy(c2) * wc1.z, pc = xy(wc1) * c2.z;
+#else
+	const V3 px = v3(c2.x * wc1.x, c2.y * wc1.x, 0), py = v3(c2.x * wc1.y, c2.y * wc1.y, 0),
+			pz = v3(c2.x * wc1.z, c2.y * wc1.z, 0), pc = v3(wc1.x * c2.z, wc1.y * c2.z, 0);
+#endif
+	r[0] = px.x; r[1] = px.y; r[2] = pc.x;
+	r[3] = py.x; r[4] = py.y; r[5] = pc.y;
+	r[6] = pz.x; r[7] = pz.y; r[8] = wc1.z * c2.z;
 	r[9] = dot(wc1, c1);
 	r[10] = dot(c2, c2);
+}
+// One heading's terms added to QCP::inner_product's sums (qcp.cpp:162-218): float products
+// (packed as in qcp_terms), each widened and added to its fp64 sum in the reference's order.
+__device__ __forceinline__ void qcp_accumulate(QSums &S, const V3 wc1, const V3 c1, const V3 c2, double w) {
+	S.ss1 += (double)dot(wc1, c1);
+	S.ss2 += w * (double)dot(c2, c2);
+#ifdef GD_PACK
+	const F2 px = xy(c2) * wc1.x, py = xy(c2) * wc1.y, pz = xy(c2) * wc1.z, pc = xy(wc1) * c2.z;
+#else
+	const V3 px = v3(c2.x * wc1.x, c2.y * wc1.x, 0), py = v3(c2.x * wc1.y, c2.y * wc1.y, 0),
+			pz = v3(c2.x * wc1.z, c2.y * wc1.z, 0), pc = v3(wc1.x * c2.z, wc1.y * c2.z, 0);
+#endif
+	S.xx += (double)px.x;
+	S.xy += (double)px.y;
+	S.xz += (double)pc.x;
+	S.yx += (double)py.x;
+	S.yy += (double)py.y;
+	S.yz += (double)pc.y;
+	S.zx += (double)pz.x;
+	S.zy += (double)pz.y;
+	S.zz += (double)(wc1.z * c2.z);
 }
 // STAB: the plan has stabilization passes (a separate instantiation keeps the retry loop and
 // its LDS staging out of the default kernel).
@@ -954,7 +999,7 @@ __device__ __forceinline__ void qcp_terms(const V3 wc1, const V3 c1, const V3 c2
 // HELP: the parent-side values come from the helper wave's record hrec (kHelpF4 float4 at
 // stride 64), not from this wave.  XS: the build serves split-exchange tasks (xs, staging 4 /
 // 5): only the two-waves-per-SIMD build, so that the one-wave kernels keep their registers.
-template <bool STAB, bool PR, int TA, bool HELP, bool XS, class LV, class GV, class FP, class IP>
+template <bool STAB, bool PR, int TA, bool HELP, bool XS, int PM, class LV, class GV, class FP, class IP>
 __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, int xs, size_t s, const LV &L, const GV &G, const FP TG,
 		const FP ST, const IP SF, const FP HS, const FP OE, const FP MS, double &prev_dev, const EffPre &pre, bool hoist,
 		const float4 *hrec, int *hfl, int hseq, bool *hstuck MBIK_PROF_PARAM) {
@@ -1010,8 +1055,8 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, int xs
 	Headings H;
 	if (nh == 1) {
 		// one heading in the segment: every lane of the group computes it (qcp.cpp:59-78)
-		if (hoist) effector_headings(t, pre, d0, Gb, L, ST, SF, H, OE, oe_mode);
-		else effector_headings<TA>(t, t.seg_effs[e0], d0, Gb, L, TG, ST, SF, s, hw, H, OE, oe_mode);
+		if (hoist) effector_headings<PM>(t, pre, d0, Gb, L, ST, SF, H, OE, oe_mode);
+		else effector_headings<TA, PM>(t, t.seg_effs[e0], d0, Gb, L, TG, ST, SF, s, hw, H, OE, oe_mode);
 		V3 mvd = H.hm[0], tgt = H.ht[0];
 		if (translate) {
 			double w = H.w[0];
@@ -1051,9 +1096,9 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, int xs
 				Headings Hm;
 				if (i < e1 && pass == 2) {
 					EffPre p;
-					load_eff<TA>(t, t.seg_effs[i], TG, s, hw + t.seg_eff_hoff[i], p);
+					load_eff<TA, PM>(t, t.seg_effs[i], TG, s, hw + t.seg_eff_hoff[i], p);
 					const X3 E = ld_x(xe + 12 * r);
-					heading_terms(p, E, E.o, Gb.o, Hm);
+					heading_terms<PM>(p, E, E.o, Gb.o, Hm);
 				} else if (i < e1) {
 					int lc[2] = {0, 0};
 					if (i - m >= e0) {
@@ -1065,13 +1110,13 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, int xs
 						for (int u = i + 2; u <= i + m; u++) lc[1] = min(lc[1], t.seg_eff_lcp[u]);
 					}
 					X3 E;
-					effector_headings<TA>(t, t.seg_effs[i], d0, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], Hm, OE, oe_mode,
+					effector_headings<TA, PM>(t, t.seg_effs[i], d0, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], Hm, OE, oe_mode,
 							PR ? &pc : nullptr, lc, pass == 1 ? &E : nullptr);
 					if (pass == 1) st_x(xe + 12 * r, E);
 				}
 				for (int v = 0; v < m && i0 + v < e1; v++) {
 					Headings H; // (weights and mask only)
-					heading_weights(t, t.seg_effs[i0 + v], hw + t.seg_eff_hoff[i0 + v], H);
+					heading_weights<PM>(t, t.seg_effs[i0 + v], hw + t.seg_eff_hoff[i0 + v], H);
 					const int src = lb + v;
 #pragma unroll
 					for (int h = 0; h < 7; h++) {
@@ -1104,18 +1149,7 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, int xs
 		each([&](V3 ht, V3 hm, double w) __attribute__((always_inline)) {
 			V3 c1 = translate ? ht + ntc : ht;
 			V3 c2 = translate ? hm + nmc : hm;
-			V3 wc1 = c1 * (float)w;
-			S.ss1 += (double)dot(wc1, c1);
-			S.ss2 += w * (double)dot(c2, c2);
-			S.xx += (double)(wc1.x * c2.x);
-			S.xy += (double)(wc1.x * c2.y);
-			S.xz += (double)(wc1.x * c2.z);
-			S.yx += (double)(wc1.y * c2.x);
-			S.yy += (double)(wc1.y * c2.y);
-			S.yz += (double)(wc1.y * c2.z);
-			S.zx += (double)(wc1.z * c2.x);
-			S.zy += (double)(wc1.z * c2.y);
-			S.zz += (double)(wc1.z * c2.z);
+			qcp_accumulate(S, c1 * (float)w, c1, c2, w);
 		}, kXE && translate ? 2 : 0);
 		qrot = qcp_adjugate(S);
 	} else if (m == 1 || nh == 0) {
@@ -1131,8 +1165,8 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, int xs
 			PathCk pc;
 			pc.d = -1;
 			for (int i = e0; i < e1; i++) {
-				if (hoist) effector_headings(t, pre, d0, Gb, L, ST, SF, H, OE, oe_mode);
-				else effector_headings<TA>(t, t.seg_effs[i], d0, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, oe_mode,
+				if (hoist) effector_headings<PM>(t, pre, d0, Gb, L, ST, SF, H, OE, oe_mode);
+				else effector_headings<TA, PM>(t, t.seg_effs[i], d0, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, oe_mode,
 						PR ? &pc : nullptr, t.seg_eff_lcp + i);
 #pragma unroll
 				for (int h = 0; h < 7; h++) {
@@ -1155,8 +1189,8 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, int xs
 		pc.d = -1;
 		for (int i = e0; i < e1; i++) {
 			MBIK_PROF_T(ph1);
-			if (hoist) effector_headings(t, pre, d0, Gb, L, ST, SF, H, OE, oe_mode);
-			else effector_headings<TA>(t, t.seg_effs[i], d0, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, oe_mode,
+			if (hoist) effector_headings<PM>(t, pre, d0, Gb, L, ST, SF, H, OE, oe_mode);
+			else effector_headings<TA, PM>(t, t.seg_effs[i], d0, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, oe_mode,
 					PR ? &pc : nullptr, t.seg_eff_lcp + i);
 			MBIK_PROF_T(ph2);
 			MBIK_PROF_ADD(9, ph1, ph2);
@@ -1166,18 +1200,7 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, int xs
 					const double w = H.w[h];
 					V3 c1 = translate ? H.ht[h] + ntc : H.ht[h];
 					V3 c2 = translate ? H.hm[h] + nmc : H.hm[h];
-					V3 wc1 = c1 * (float)w;
-					S.ss1 += (double)dot(wc1, c1);
-					S.ss2 += w * (double)dot(c2, c2);
-					S.xx += (double)(wc1.x * c2.x);
-					S.xy += (double)(wc1.x * c2.y);
-					S.xz += (double)(wc1.x * c2.z);
-					S.yx += (double)(wc1.y * c2.x);
-					S.yy += (double)(wc1.y * c2.y);
-					S.yz += (double)(wc1.y * c2.z);
-					S.zx += (double)(wc1.z * c2.x);
-					S.zy += (double)(wc1.z * c2.y);
-					S.zz += (double)(wc1.z * c2.z);
+					qcp_accumulate(S, c1 * (float)w, c1, c2, w);
 				}
 			}
 			MBIK_PROF_T(ph6);
@@ -1203,7 +1226,7 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, int xs
 		const auto ex = rebind<double>(hsg + HS_REC * nh);
 		for (int i = e0 + j; i < e1; i += m) {
 			MBIK_PROF_T(ph1);
-			effector_headings<TA>(t, t.seg_effs[i], d0, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, oe_mode);
+			effector_headings<TA, PM>(t, t.seg_effs[i], d0, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, oe_mode);
 			MBIK_PROF_T(ph2);
 			MBIK_PROF_ADD(9, ph1, ph2);
 			auto r = hsg + HS_REC * t.seg_eff_hoff[i];
@@ -1392,7 +1415,7 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, int xs
 		Headings H;
 		const double *hw = t.seg_hw + t.seg_hw_off[seg];
 		for (int i = t.seg_eff_off[seg] + j; i < t.seg_eff_off[seg + 1]; i += m)
-			effector_headings<TA>(t, t.seg_effs[i], d0, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, 1);
+			effector_headings<TA, PM>(t, t.seg_effs[i], d0, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, 1);
 	}
 
 	MBIK_PROF_T(pt2);
@@ -1477,7 +1500,7 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, int xs
 		Headings H;
 		for (int i = t.seg_eff_off[seg] + j; i < t.seg_eff_off[seg + 1]; i += m) {
 			const int e = t.seg_effs[i];
-			effector_headings<TA>(t, e, d0, Gnow, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, 2);
+			effector_headings<TA, PM>(t, e, d0, Gnow, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, 2);
 #pragma unroll
 			for (int h = 0; h < 7; h++) {
 				if (H.mask & (1 << h)) {
@@ -1621,7 +1644,7 @@ __device__ __forceinline__ int row_steps(const DevPlan &t, int r, int seg_lo, in
 	return __builtin_amdgcn_readfirstlane(n);
 }
 
-template <bool STAB, int PL, bool HOIST = true, bool T32 = true, bool HELP = false, bool XS = false>
+template <bool STAB, int PL, bool HOIST = true, bool T32 = true, bool HELP = false, bool XS = false, int PM = 0>
 __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int count, const float *__restrict__ pose_in,
 		const float *__restrict__ targets, float *__restrict__ pose_out, int iterations, int seg_lo, int seg_hi) {
 	static_assert(!HELP || (!STAB && PL == 0), "the helper wave serves placement-0 launches without stabilization");
@@ -1803,8 +1826,8 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 					if (rp) hrec = rp + (size_t)seq * kHelpF4 * 64;
 #endif
 					if (k0 + q < k1)
-						bone_step<false, true, kTab32, true, false>(t, seg, k0 + q, task.y, task.z, task.w & mbik::SCHED_XS, s, L, G, TG, ST, SF, HS, OE, MS, prev_dev,
-								pre, hoist, hrec, b_ready ? nullptr : hfl, seq, &stuck MBIK_PROF_ARG);
+						bone_step<false, true, kTab32, true, false, PM>(t, seg, k0 + q, task.y, task.z, task.w & mbik::SCHED_XS, s, L, G, TG, ST,
+								SF, HS, OE, MS, prev_dev, pre, hoist, hrec, b_ready ? nullptr : hfl, seq, &stuck MBIK_PROF_ARG);
 					help_post(hfl + 2, seq + 1);
 					slot = slot + 1 == kHelpSlots ? 0 : slot + 1;
 				}
@@ -1856,8 +1879,8 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 					}
 				}
 				if (k >= ke) break;
-				bone_step<STAB, HOIST || PL == 2, TA, false, XS>(t, seg, k, task.y, task.z,
-						task.w & mbik::SCHED_XS, s, L, G, TG, ST, SF, HS, OE, MS, prev_dev, pre, hoist, nullptr, nullptr, 0, nullptr MBIK_PROF_ARG);
+				bone_step<STAB, HOIST || PL == 2, TA, false, XS, PM>(t, seg, k, task.y, task.z, task.w & mbik::SCHED_XS, s, L, G, TG, ST, SF,
+						HS, OE, MS, prev_dev, pre, hoist, nullptr, nullptr, 0, nullptr MBIK_PROF_ARG);
 				k++;
 			}
 			__syncthreads();
@@ -1904,26 +1927,30 @@ __device__ __forceinline__ int xcd_block() {
 // whose state is not in LDS (mbik_plan_set_waves_per_simd; autotune decides).
 // XS: the build with split-exchange segments (staging 4 / 5; two waves per SIMD only), a separate
 // instantiation so the other builds keep their register allocation.
-template <bool STAB, int PL, int WPE = MBIK_WAVES_PER_EU, bool T32 = true, bool XS = false>
+// PM: kPrioDefault for plans whose effectors all have the reference's default priorities
+// (DevPlan::prio_mask), a separate instantiation with compile-time heading slots; else 0.
+template <bool STAB, int PL, int WPE = MBIK_WAVES_PER_EU, bool T32 = true, bool XS = false, int PM = 0>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void mbik_solve_kernel(DevPlan t, int first, int count, const float *__restrict__ pose_in,
 		const float *__restrict__ targets, float *__restrict__ pose_out, int iterations, int seg_lo, int seg_hi) {
-	solve_block<STAB, PL, WPE == 1, T32, false, XS>(t, xcd_block(), first, count, pose_in, targets, pose_out, iterations, seg_lo, seg_hi);
+	solve_block<STAB, PL, WPE == 1, T32, false, XS, PM>(t, xcd_block(), first, count, pose_in, targets, pose_out, iterations, seg_lo, seg_hi);
 }
 
 // The same with a helper wave (two waves per block, on two SIMDs of a CU): placement 0, no
 // stabilization, 32-bit table addressing (mbik_plan_set_helper_wave; autotune decides).
+template <int PM>
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(1, 1))) void mbik_solve_kernel_help(DevPlan t, int first, int count,
 		const float *__restrict__ pose_in, const float *__restrict__ targets, float *__restrict__ pose_out, int iterations, int seg_lo,
 		int seg_hi) {
-	solve_block<false, 0, true, true, true>(t, xcd_block(), first, count, pose_in, targets, pose_out, iterations, seg_lo, seg_hi);
+	solve_block<false, 0, true, true, true, false, PM>(t, xcd_block(), first, count, pose_in, targets, pose_out, iterations, seg_lo, seg_hi);
 }
 
 #ifdef MBIK_REPLAY
 // The solving wave alone, replaying saved helper records (diagnostic build only).
+template <int PM>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void mbik_solve_kernel_replay(DevPlan t, int first, int count,
 		const float *__restrict__ pose_in, const float *__restrict__ targets, float *__restrict__ pose_out, int iterations, int seg_lo,
 		int seg_hi) {
-	solve_block<false, 0, true, true, true>(t, xcd_block(), first, count, pose_in, targets, pose_out, iterations, seg_lo, seg_hi);
+	solve_block<false, 0, true, true, true, false, PM>(t, xcd_block(), first, count, pose_in, targets, pose_out, iterations, seg_lo, seg_hi);
 }
 #endif
 
@@ -2181,19 +2208,28 @@ SolveKernel solve_kernel_for(const mbik_plan *p) {
 	// placement 0 with tables of 4 GiB or more: 64-bit element indices
 	static const SolveKernel k64[3] = {mbik_solve_kernel<false, 0, 1, false>, mbik_solve_kernel<true, 0, 1, false>,
 			mbik_solve_kernel<false, 0, 2, false>};
+	// the default-priority instantiations (PM = kPrioDefault) of the non-stabilized 32-bit builds
+	constexpr int D = kPrioDefault;
+	static const SolveKernel kd[3] = {mbik_solve_kernel<false, 0, 1, true, false, D>, mbik_solve_kernel<false, 1, 1, true, false, D>,
+			mbik_solve_kernel<false, 2, 1, true, false, D>};
+	static const SolveKernel k2d[3] = {mbik_solve_kernel<false, 0, 2, true, false, D>, mbik_solve_kernel<false, 1, 2, true, false, D>,
+			mbik_solve_kernel<false, 2, 2, true, false, D>};
+	static const SolveKernel k2xd[3] = {mbik_solve_kernel<false, 0, 2, true, true, D>, mbik_solve_kernel<false, 1, 2, true, true, D>,
+			mbik_solve_kernel<false, 2, 2, true, true, D>};
 	static std::once_flag once;
 	std::call_once(once, [] {
 		for (auto &row : ks)
 			for (SolveKernel k : row) (void)hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-		for (SolveKernel k : k2) (void)hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-		for (SolveKernel k : k2x) (void)hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-		for (SolveKernel k : k64) (void)hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+		for (const SolveKernel *a : {k2, k2x, k64, kd, k2d, k2xd})
+			for (int i = 0; i < 3; i++) (void)hipFuncSetAttribute((const void *)a[i], hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 	});
 	const int pl = std::min(2, std::max(0, (int)h.state_hbm));
 	const bool two = h.waves_per_simd == 2 && h.stabilization_passes == 0;
 	if (pl == 0 && !tables_fit_32(p)) return two ? k64[2] : k64[h.stabilization_passes > 0 ? 1 : 0];
-	if (two) return h.has_xs ? k2x[pl] : k2[pl];
-	return ks[h.stabilization_passes > 0 ? 1 : 0][pl];
+	const bool dflt = p->dev.prio_mask == kPrioDefault;
+	if (two) return h.has_xs ? (dflt ? k2xd[pl] : k2x[pl]) : (dflt ? k2d[pl] : k2[pl]);
+	if (h.stabilization_passes > 0) return ks[1][pl];
+	return dflt ? kd[pl] : ks[0][pl];
 }
 
 // Whether a launch of the plan's current layout runs with the helper wave
@@ -2573,19 +2609,23 @@ int launch(mbik_plan *p, int first, int count, const float *pose_in, const float
 	if (helper_on(p)) {
 		static std::once_flag honce;
 		std::call_once(honce, [] {
-			(void)hipFuncSetAttribute((const void *)mbik_solve_kernel_help, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+			(void)hipFuncSetAttribute((const void *)mbik_solve_kernel_help<0>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+			(void)hipFuncSetAttribute((const void *)mbik_solve_kernel_help<kPrioDefault>, hipFuncAttributeMaxDynamicSharedMemorySize,
+					160 * 1024);
 		});
 		if ((rc = ensure_help_flag(p)) != MBIK_OK) return rc;
-		kern = mbik_solve_kernel_help;
+		kern = p->dev.prio_mask == kPrioDefault ? mbik_solve_kernel_help<kPrioDefault> : mbik_solve_kernel_help<0>;
 		lds += kHelpRingBytes;
 		threads = 128;
 #ifdef MBIK_REPLAY
 		if (p->dev.replay == 2) {
 			static std::once_flag ronce;
 			std::call_once(ronce, [] {
-				(void)hipFuncSetAttribute((const void *)mbik_solve_kernel_replay, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+				(void)hipFuncSetAttribute((const void *)mbik_solve_kernel_replay<0>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+				(void)hipFuncSetAttribute((const void *)mbik_solve_kernel_replay<kPrioDefault>, hipFuncAttributeMaxDynamicSharedMemorySize,
+						160 * 1024);
 			});
-			kern = mbik_solve_kernel_replay;
+			kern = p->dev.prio_mask == kPrioDefault ? mbik_solve_kernel_replay<kPrioDefault> : mbik_solve_kernel_replay<0>;
 			threads = 64;
 		}
 #endif
@@ -2712,6 +2752,18 @@ int finish_plan(mbik_plan *p, const float *setup_pose, const void *cm_state) {
 	d.stab = h.stabilization_passes; d.constraint_mode = h.constraint_mode; d.hs_floats = h.hs_floats;
 	d.libm = h.libm_variant;
 	d.n_gck = h.n_gck;
+	// One heading slot mask shared by every effector -- the reference's default priorities, the
+	// usual case -- runs bone-steps specialised for it (kPrioDefault).
+	{
+		int pm = -1;
+		for (int e = 0; e < h.P && pm != 0; e++) {
+			int m = 1;
+			for (int a = 0; a < 3; a++)
+				if (h.eff_prio[3 * e + a] > 0.0f) m |= 6 << (2 * a);
+			pm = pm < 0 || pm == m ? m : 0;
+		}
+		d.prio_mask = pm == kPrioDefault ? pm : 0;
+	}
 	d.lds_stride = (mbik::lds_floats_per_skeleton(h) + 3) & ~3;
 	int rc = 0;
 	rc = rc ? rc : upload(p, h.D, d.D);
@@ -3243,6 +3295,7 @@ int32_t mbik_plan_get_info(const mbik_plan *p, mbik_plan_info *o) {
 	o->cd_stride = h.cd_stride();
 	o->libm_variant = h.libm_variant;
 	o->helper_wave = helper_on(p) ? 1 : 0;
+	o->heading_slots = p->dev.prio_mask;
 	return MBIK_OK;
 }
 

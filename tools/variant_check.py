@@ -4,6 +4,8 @@ batches of C1-C5, then kernel time per config.  Each variant runs in its own pro
 tags are interleaved over `--reps` rounds so that clock drift hits every variant alike.
 
     python tools/variant_check.py [--reps 2] [--cases 2:4096,3:65536] TAG [TAG ...]
+A case is CFG:N (autotuned per variant) or CFG:N:K:spw:interval:staging:placement:waves[:helper]
+(a pinned layout, as bench.py --layout).
 """
 from __future__ import annotations
 
@@ -37,13 +39,23 @@ def child(tag: str, cases: str, parity: bool):
             ok[f"c{cfg}"] = bool(np.array_equal(got.view(np.uint32), ref.view(np.uint32)))
         out["bitwise"] = ok
     for case in cases.split(","):
-        cfg, n = (int(x) for x in case.split(":"))
+        f = [int(x) for x in case.split(":")]
+        cfg, n = f[:2]
         wl = W.generate(cfg, n)
         p = Plan.from_workload(wl)
         pi = torch.from_numpy(wl.pose).to(dev)
         tg = torch.from_numpy(wl.targets).to(dev)
         po_ = torch.empty_like(pi)
-        p.autotune(pi.data_ptr(), tg.data_ptr(), po_.data_ptr(), 0, n, st)
+        if len(f) >= 8:
+            # pinned layout CFG:N:K:spw:interval:staging:placement:waves[:helper] (bench.py --layout)
+            k, spw, interval, staging, placement, waves = f[2:8]
+            p.set_helper_wave(f[8] if len(f) > 8 else 0)
+            p.set_layout(k, spw, interval)
+            p.set_heading_staging(staging)
+            p.set_locals_placement(placement)
+            p.set_waves_per_simd(waves)
+        else:
+            p.autotune(pi.data_ptr(), tg.data_ptr(), po_.data_ptr(), 0, n, st)
         for _ in range(2):
             p.solve(pi.data_ptr(), tg.data_ptr(), po_.data_ptr(), 0, n, st)
         e0 = torch.cuda.Event(enable_timing=True)
