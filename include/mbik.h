@@ -398,7 +398,9 @@ int32_t mbik_selftest_div(int32_t device, uint64_t random_iterations, uint64_t o
  *   COS_F64              cos(x): tangent-radius cosines (ik_open_cone_3d.cpp:36-120)
  *   SINF_SSE2, COSF_SSE2, SLERP_SCALE0_SSE2   the same for a plan created with
  *                        libm_variant = MBIK_LIBM_VARIANT_SSE2 (compare with a host libm
- *                        whose FMA ifunc is disabled: GLIBC_TUNABLES=glibc.cpu.hwcaps=-FMA,-AVX2_Usable) */
+ *                        whose FMA ifunc is disabled: GLIBC_TUNABLES=glibc.cpu.hwcaps=-FMA,-AVX2_Usable)
+ *   ACOSF_UNIT           the slerp's acosf call site: the branch-free form for -0.5 < x < 1,
+ *                        acosf elsewhere; compare with the host acosf */
 #define MBIK_LIBM_SINF 0
 #define MBIK_LIBM_COSF 1
 #define MBIK_LIBM_ACOSF 2
@@ -408,6 +410,7 @@ int32_t mbik_selftest_div(int32_t device, uint64_t random_iterations, uint64_t o
 #define MBIK_LIBM_SINF_SSE2 6
 #define MBIK_LIBM_COSF_SSE2 7
 #define MBIK_LIBM_SLERP_SCALE0_SSE2 8
+#define MBIK_LIBM_ACOSF_UNIT 9
 int32_t mbik_selftest_libm(int32_t fn, uint64_t first, uint64_t count, const double *inputs, const void *expected,
 		uint64_t out[3], void *hip_stream);
 

@@ -20,7 +20,7 @@ MBIK_ENODEV = -5
 
 # mbik_selftest_libm function codes (include/mbik.h)
 LIBM_SINF, LIBM_COSF, LIBM_ACOSF, LIBM_SLERP_SCALE0, LIBM_COS_F64_OF_F32, LIBM_COS_F64, LIBM_SINF_SSE2, LIBM_COSF_SSE2, \
-    LIBM_SLERP_SCALE0_SSE2 = range(9)
+    LIBM_SLERP_SCALE0_SSE2, LIBM_ACOSF_UNIT = range(10)
 # mbik_plan_options.libm_variant: the reference host's glibc sinf/cosf build
 LIBM_VARIANT_FMA, LIBM_VARIANT_SSE2 = 0, 1
 # a process's environment that makes ITS glibc pick the SSE2 build (the reference host of LIBM_VARIANT_SSE2)

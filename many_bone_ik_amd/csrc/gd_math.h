@@ -292,6 +292,52 @@ GDI float acosf(float x) {
 	const float w = r * s + cc;
 	return 2.0f * (df + w);
 }
+// sinf for |y| <= 1.6 (the slerp coefficient's omega), branch-free: the same operations as
+// sincosf above on each path -- below |y| = 0.75 the reduction's n is 0, so x - 0 * (pi/2) is
+// x exactly and the reduced path computes what the direct one does -- with both polynomials
+// evaluated and the result selected, so lanes on different paths do not run them in turn.
+template <bool FMA>
+GDI float sinf_small(float y) {
+	const double x = y;
+	const double r = x * kHalfPiInv24;
+	const int n = ((int32_t)r + 0x800000) >> 24;
+	const double xr = FMA ? fma(-(double)n, kHalfPi, x) : x - (double)n * kHalfPi;
+	const double xs = ((n + 1) & 2) ? -xr : xr;
+	const float sp = sin_poly<FMA>(xs, xs * xs);
+	const float cp = cos_poly<FMA>(xs * xs);
+	const float v = (n & 1) == 0 ? sp : ((n & 2) ? -cp : cp);
+	return top12(y) < 0x398u ? y : v;
+}
+// acosf for 0 <= x < 1 (the slerp's cosine of the half angle), branch-free: both of acosf's
+// paths for that range share one rational approximation at their own z.
+GDI float acosf_unit(float x) {
+	constexpr float pio2_hi = 1.5707962513e+00f, pio2_lo = 7.5497894159e-08f;
+	constexpr float pS0 = 1.6666667163e-01f, pS1 = -3.2556581497e-01f, pS2 = 2.0121252537e-01f, pS3 = -4.0055535734e-02f,
+					pS4 = 7.9153501429e-04f, pS5 = 3.4793309169e-05f;
+	constexpr float qS1 = -2.4033949375e+00f, qS2 = 2.0209457874e+00f, qS3 = -6.8828397989e-01f, qS4 = 7.7038154006e-02f;
+	union {
+		float f;
+		int32_t i;
+	} c{x};
+	const int32_t ix = c.i & 0x7fffffff;
+	const bool lo = ix < 0x3f000000; // |x| < 0.5
+	const float z = lo ? x * x : (1.0f - x) * 0.5f;
+	const float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+	const float q = 1.0f + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+	const float r = p / q;
+	const float a = pio2_hi - (x - (pio2_lo - x * r));
+	const float s = gd_sqrt(z);
+	union {
+		float f;
+		uint32_t u;
+	} d{s};
+	d.u &= 0xfffff000u;
+	const float df = d.f;
+	const float cc = (z - df * df) / (s + df);
+	const float w = r * s + cc;
+	const float h = 2.0f * (df + w);
+	return ix <= 0x32800000 ? pio2_hi + pio2_lo : (lo ? a : h);
+}
 } // namespace glibc
 
 // Which glibc build the reference host's sinf/cosf are (the plan's libm_variant,
@@ -334,14 +380,14 @@ GDI double sin_taylor(double x) {
 	return fma(x * x2, p, x);
 }
 GDI float slerp_scale0(float omega, int lv = LIBM_FMA) {
-	const float sinom = sin_f(omega, lv);
 	if (fabsf(omega) <= 1.6f) {
+		const float sinom = lv == LIBM_SSE2 ? glibc::sinf_small<false>(omega) : glibc::sinf_small<true>(omega);
 		const double q = sin_taylor((double)omega) * gd_rcp(sinom).r;
 		const double w = fabs(q) * 0x1p-46;
 		const float lo = (float)(q - w), hi = (float)(q + w);
 		if (lo == hi) return lo; // (a NaN estimate, sinom == 0, falls through)
 	}
-	return (float)(sin((double)omega) / (double)sinom);
+	return (float)(sin((double)omega) / (double)sin_f(omega, lv));
 }
 #else
 GDI float slerp_scale0(float omega, int lv = LIBM_FMA) {

@@ -404,7 +404,7 @@ __device__ __forceinline__ B3 slerp_weight0(const B3 &from_b, const SlerpTo &tt,
 	float scale0, scale1;
 	if ((1.0f - cosom) > (float)CMP_EPSILON) {
 		// scale1 = sinf(0 * omega) / sinom is +0 for the finite omega of this branch
-		scale0 = slerp_scale0(acos_f(cosom), lv);
+		scale0 = slerp_scale0(glibc::acosf_unit(cosom), lv); // 0 <= cosom < 1 - CMP_EPSILON here
 		scale1 = 0.0f;
 	} else {
 		scale0 = 1.0f;
@@ -3846,7 +3846,8 @@ __global__ void mbik_selftest_libm_kernel(int fn, uint64_t first, uint64_t count
 			const float e = static_cast<const float *>(expected)[i];
 			const float g = fn == MBIK_LIBM_SINF ? sin_f(x) : fn == MBIK_LIBM_COSF ? cos_f(x) : fn == MBIK_LIBM_ACOSF ? acos_f(x)
 					: fn == MBIK_LIBM_SLERP_SCALE0 ? slerp_scale0(x) : fn == MBIK_LIBM_SINF_SSE2 ? sin_f(x, LIBM_SSE2)
-					: fn == MBIK_LIBM_COSF_SSE2 ? cos_f(x, LIBM_SSE2) : slerp_scale0(x, LIBM_SSE2);
+					: fn == MBIK_LIBM_COSF_SSE2 ? cos_f(x, LIBM_SSE2) : fn == MBIK_LIBM_SLERP_SCALE0_SSE2 ? slerp_scale0(x, LIBM_SSE2)
+					: (x > -0.5f && x < 1.0f) ? glibc::acosf_unit(x) : acos_f(x); // MBIK_LIBM_ACOSF_UNIT
 			ok = exact = same_bits(e, g);
 		} else {
 			const double e = static_cast<const double *>(expected)[i];
@@ -3923,7 +3924,7 @@ int32_t mbik_selftest_div(int32_t device, uint64_t random_iterations, uint64_t o
 int32_t mbik_selftest_libm(int32_t fn, uint64_t first, uint64_t count, const double *inputs, const void *expected,
 		uint64_t out[3], void *hip_stream) {
 	if (!out || !expected) return fail(MBIK_EINVAL, "null argument");
-	if (fn < MBIK_LIBM_SINF || fn > MBIK_LIBM_SLERP_SCALE0_SSE2) return fail(MBIK_EINVAL, "unknown function code");
+	if (fn < MBIK_LIBM_SINF || fn > MBIK_LIBM_ACOSF_UNIT) return fail(MBIK_EINVAL, "unknown function code");
 	if (fn == MBIK_LIBM_COS_F64 ? !inputs : first + count > (1ull << 32)) return fail(MBIK_EINVAL, "input range");
 	out[0] = 0;
 	out[1] = ~0ull;

@@ -5,7 +5,9 @@ gd_math.h restates glibc's float algorithms for the device and uses the device's
 sin/cos, so each call site is proven equal here:
   sin_f, cos_f, acos_f         all 2^32 float inputs
   slerp_scale0                 all 2^32 omega: (float)(sin((double)w) / (double)sinf(w)),
-                               Quaternion::slerp's weight-0 coefficient (ik_bone_segment_3d.cpp:148-151)
+                               Quaternion::slerp's weight-0 coefficient (ik_bone_segment_3d.cpp:148-151);
+                               its sinf is the branch-free glibc::sinf_small for |w| <= 1.6
+  acosf_unit                   all 2^32 x: the slerp's acosf call site (branch-free for -0.5 < x < 1)
   cos((double)x)               all 2^32 float x: the cone radius cosines (setup)
   cos(x), x double             2^26 random tangent-radius-like doubles (setup; not enumerable)
 The device's double cos (OCML) is not glibc's: it differs in the last bit on ~1.6 % of the
@@ -27,11 +29,11 @@ CHUNK = 1 << 26
 THREADS = max(1, min(16, len(os.sched_getaffinity(0))))
 
 
-def _check(mbik, oracle, fn, first, count, inputs=None):
+def _check(mbik, oracle, fn, first, count, inputs=None, exp_fn=None):
     import ctypes
     import torch
     dev = torch.device("cuda", 0)
-    exp = torch.from_numpy(oracle.libm_fill(fn, first, count, inputs, threads=THREADS)).to(dev)
+    exp = torch.from_numpy(oracle.libm_fill(fn if exp_fn is None else exp_fn, first, count, inputs, threads=THREADS)).to(dev)
     inp = torch.from_numpy(inputs).to(dev) if inputs is not None else None
     out = (ctypes.c_uint64 * 3)()
     rc = mbik.mbik_selftest_libm(fn, first, count, inp.data_ptr() if inp is not None else None, exp.data_ptr(), out,
@@ -42,11 +44,14 @@ def _check(mbik, oracle, fn, first, count, inputs=None):
 
 @pytest.mark.parametrize("fn,name", [(_lib.LIBM_SINF, "sinf"), (_lib.LIBM_COSF, "cosf"), (_lib.LIBM_ACOSF, "acosf"),
                                      (_lib.LIBM_SLERP_SCALE0, "slerp_scale0"),
-                                     (_lib.LIBM_COS_F64_OF_F32, "cos_f64_of_f32")])
+                                     (_lib.LIBM_COS_F64_OF_F32, "cos_f64_of_f32"),
+                                     (_lib.LIBM_ACOSF_UNIT, "acosf_unit")])
 def test_all_float_inputs(mbik, oracle, fn, name):
+    # acosf_unit: the slerp's branch-free acosf (gd_math.h glibc::acosf_unit), against the host acosf
+    exp_fn = _lib.LIBM_ACOSF if fn == _lib.LIBM_ACOSF_UNIT else None
     bad_total, first_bad, bits = 0, None, 0
     for first in range(0, 1 << 32, CHUNK):
-        bad, lo, diff = _check(mbik, oracle, fn, first, CHUNK)
+        bad, lo, diff = _check(mbik, oracle, fn, first, CHUNK, exp_fn=exp_fn)
         if bad and first_bad is None:
             first_bad = first + lo
         bad_total += bad
@@ -72,6 +77,6 @@ def test_cos_double_sample(mbik, oracle):
 def test_selftest_libm_rejects_bad_arguments(mbik):
     import ctypes
     out = (ctypes.c_uint64 * 3)()
-    assert mbik.mbik_selftest_libm(9, 0, 1, None, None, out, None) == _lib.MBIK_EINVAL
+    assert mbik.mbik_selftest_libm(10, 0, 1, None, None, out, None) == _lib.MBIK_EINVAL
     assert mbik.mbik_selftest_libm(_lib.LIBM_SINF, 1 << 32, 1, None, ctypes.c_void_p(8), out, None) == _lib.MBIK_EINVAL
     assert mbik.mbik_selftest_libm(_lib.LIBM_COS_F64, 0, 1, None, ctypes.c_void_p(8), out, None) == _lib.MBIK_EINVAL

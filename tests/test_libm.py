@@ -81,3 +81,20 @@ def test_product_libm_variants_match_their_glibc_build(variant, sse2_platform):
     assert all(v == 0 for v in _run_checker(variant, sse2_platform, "list", *disc).values())
     crossed = _run_checker(1 - variant, sse2_platform, "list", *disc)
     assert crossed["sin_f"] == 4 and crossed["cos_f"] == 4 and crossed["acos_f"] == 0
+
+
+def test_branch_free_slerp_forms_match_glibc_restatements():
+    """tools/branchfree_check.cpp: gd_math.h's branch-free sinf (|y| <= 1.6) and acosf
+    (-0.5 < x < 1), used by the solve's slerp coefficient, against the branchy restatements on
+    every 97th float of their ranges (the full ranges and the device: tests/test_gpu_libm.py)."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "build", "branchfree_check_test")
+    src = os.path.join(root, "tools", "branchfree_check.cpp")
+    os.makedirs(os.path.dirname(exe), exist_ok=True)
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-fno-builtin", "-pthread", "-I",
+                    os.path.join(root, "many_bone_ik_amd", "csrc"), src, "-o", exe], check=True)
+    out = subprocess.run([exe, "97"], capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "FMA mismatches 0, SSE2 mismatches 0; acosf_unit mismatches 0" in out.stdout
