@@ -466,6 +466,21 @@ GDI V3 normalized(V3 a) {
 	const GdRcp d = gd_sqrt_rcp(l, len);
 	return v3(gd_quot(a.x, d), gd_quot(a.y, d), gd_quot(a.z, d));
 }
+// The same with the zero-vector case selected instead of branched on (same operations, bit for
+// bit).  The one-wave builds call it where it is faster there: straight-line code for the
+// orthonormalizations.  The two-wave builds keep the branch, which costs them fewer registers.
+GDI V3 normalized_sel(V3 a) {
+	float l = length_sq(a);
+	float len;
+	const GdRcp d = gd_sqrt_rcp(l, len);
+	const V3 n = v3(gd_quot(a.x, d), gd_quot(a.y, d), gd_quot(a.z, d));
+	return l == 0 ? v3(0, 0, 0) : n;
+}
+template <bool SEL>
+GDI V3 normalized_t(V3 a) {
+	if constexpr (SEL) return normalized_sel(a);
+	else return normalized(a);
+}
 GDI bool is_zero_approx(float s) { return fabsf(s) < (float)CMP_EPSILON; }
 GDI bool is_equal_approx(float a, float b) {
 	if (a == b) return true;
@@ -477,9 +492,10 @@ GDI bool is_zero_approx(V3 a) { return is_zero_approx(a.x) && is_zero_approx(a.y
 GDI bool is_finite(V3 a) { return isfinite(a.x) && isfinite(a.y) && isfinite(a.z); }
 GDI bool is_nan3(V3 a) { return isnan(a.x) || isnan(a.y) || isnan(a.z); }
 GDI bool eq(V3 a, V3 b) { return a.x == b.x && a.y == b.y && a.z == b.z; }
+template <bool SEL = false>
 GDI V3 any_perpendicular(V3 a) {
 	V3 ax = (fabsf(a.x) <= fabsf(a.y) && fabsf(a.x) <= fabsf(a.z)) ? v3(1, 0, 0) : v3(0, 1, 0);
-	return normalized(cross(a, ax));
+	return normalized_t<SEL>(cross(a, ax));
 }
 
 // ---------------- Quaternion ----------------
@@ -547,13 +563,14 @@ GDI Q axis_angle_sq_sc(V3 axis, float sin_half, float cos_half) {
 	return q4(axis.x * s, axis.y * s, axis.z * s, cos_half);
 }
 // Quaternion(v0, v1) shortest arc (Godot 4.3: normalising form)
+template <bool SEL = false>
 GDI Q arc(V3 v0, V3 v1) {
 	const float ALMOST_ONE = 1.0f - (float)CMP_EPSILON;
-	V3 n0 = normalized(v0), n1 = normalized(v1);
+	V3 n0 = normalized_t<SEL>(v0), n1 = normalized_t<SEL>(v1);
 	float d = dot(n0, n1);
 	if (fabsf(d) > ALMOST_ONE) {
 		if (d >= 0) return qid();
-		V3 a = any_perpendicular(n0);
+		V3 a = any_perpendicular<SEL>(n0);
 		return q4(a.x, a.y, a.z, 0);
 	}
 	V3 c = cross(n0, n1);
@@ -620,14 +637,15 @@ GDI Q get_quaternion(const B3 &m) {
 	}
 }
 // Basis::orthonormalize (Gram-Schmidt on columns)
+template <bool SEL = false>
 GDI B3 orthonormalized(const B3 &b) {
 	if constexpr (kAblate & ABL_ORTHO) return b; // timing experiment only
 	V3 x = col(b, 0), y = col(b, 1), z = col(b, 2);
-	x = normalized(x);
+	x = normalized_t<SEL>(x);
 	y = (y - x * dot(x, y));
-	y = normalized(y);
+	y = normalized_t<SEL>(y);
 	z = (z - x * dot(x, z) - y * dot(y, z));
-	z = normalized(z);
+	z = normalized_t<SEL>(z);
 	return from_cols(x, y, z);
 }
 GDI float determinant(const B3 &b) {
@@ -635,8 +653,9 @@ GDI float determinant(const B3 &b) {
 	return r[0].x * (r[1].y * r[2].z - r[2].y * r[1].z) - r[1].x * (r[0].y * r[2].z - r[2].y * r[0].z) +
 			r[2].x * (r[0].y * r[1].z - r[1].y * r[0].z);
 }
+template <bool SEL = false>
 GDI Q get_rotation_quaternion(const B3 &b) {
-	B3 m = orthonormalized(b);
+	B3 m = orthonormalized<SEL>(b);
 	if (determinant(m) < 0) {
 		for (int i = 0; i < 3; i++) m.r[i] = m.r[i] * -1.0f;
 	}

@@ -464,17 +464,18 @@ __device__ __forceinline__ Q qcp_adjugate(const QSums &S) {
 	return normalized(q4((float)qx, (float)qy, (float)qz, (float)qw));
 }
 // QCP single pair (qcp.cpp:59-78)
+template <bool SEL = false>
 __device__ __forceinline__ Q qcp_single(V3 u, V3 v) {
 	double norm_product = length(u) * length(v);
 	if (norm_product == 0.0) return qid();
 	double d = dot(u, v);
 	if (d < ((2.0e-15 - 1.0) * norm_product)) {
-		V3 w = normalized(u);
+		V3 w = normalized_t<SEL>(u);
 		return normalized(q4(w.x, w.y, w.z, 0.0f));
 	}
 	double q0 = sqrt(0.5 * (1.0 + d / norm_product));
 	double coeff = 1.0 / (2.0 * q0 * norm_product);
-	V3 q = normalized(cross(v, u));
+	V3 q = normalized_t<SEL>(cross(v, u));
 	return normalized(q4((float)(coeff * q.x), (float)(coeff * q.y), (float)(coeff * q.z), (float)q0));
 }
 
@@ -693,12 +694,13 @@ __device__ __forceinline__ void heading_terms(const DevPlan &t, int e, const X3 
 // IKLimitCone3D::closest_to_cone (ik_open_cone_3d.cpp:358-381)
 // ni = input.normalized() and ncp = control_point.normalized() come in precomputed (the
 // point is the same for every cone; the control point is a per-skeleton constant).
+template <bool SEL = false>
 __device__ __forceinline__ V3 closest_to_cone(V3 ncp, float sin_half_r, float cos_half_r, double rcos, V3 ni, double &in_bounds) {
 	if ((double)dot(ni, ncp) > rcos) {
 		in_bounds = 1.0;
 		return v3(NAN, NAN, NAN);
 	}
-	V3 axis = normalized(cross(ncp, ni));
+	V3 axis = normalized_t<SEL>(cross(ncp, ni));
 	if (is_zero_approx(length_sq(axis)) || !is_finite(axis)) axis = v3(0, 1, 0);
 	Q rot_to = axis_angle_sq_sc(axis, sin_half_r, cos_half_r);
 	V3 acp = ncp;
@@ -709,6 +711,7 @@ __device__ __forceinline__ V3 closest_to_cone(V3 ncp, float sin_half_r, float co
 // IKLimitCone3D::get_on_great_tangent_triangle (ik_open_cone_3d.cpp:285-321)
 // c1xc2 = cross(cp, next cp) and the normalized edge normals a1 = n(cp x t1), a2 = n(t2 x cp),
 // b1 = n(t1 x next cp), b2 = n(next cp x t2) are per-skeleton constants from the setup.
+template <bool SEL = false>
 __device__ __forceinline__ V3 great_tangent_triangle(V3 c1xc2, V3 a1, V3 a2, V3 b1, V3 b2, V3 t1, V3 t2, float sin_half_tr,
 		float cos_half_tr, double trcos, V3 input) {
 	double c1c2dir = dot(input, c1xc2);
@@ -717,8 +720,8 @@ __device__ __forceinline__ V3 great_tangent_triangle(V3 c1xc2, V3 a1, V3 a2, V3 
 	V3 bb = c1c2dir < 0.0 ? b1 : b2;
 	if (dot(input, a) > 0 && dot(input, bb) > 0) {
 		if ((double)dot(input, tc) > trcos) {
-			V3 pn = normalized(cross(tc, input));
-			pn = normalized(pn);
+			V3 pn = normalized_t<SEL>(cross(tc, input));
+			pn = normalized_t<SEL>(pn);
 			return xform(axis_angle_sc(pn, sin_half_tr, cos_half_tr), tc);
 		}
 		return input;
@@ -732,14 +735,14 @@ __device__ __forceinline__ V3 great_tangent_triangle(V3 c1xc2, V3 a1, V3 a2, V3 
 // reading the basis at each step is faster: C3 -1 %, C4 -1.6 %, C5 -3 % (same-box A/B).  The
 // one-wave build keeps the whole per-segment effector data (`hoist` in solve_block).
 // IKKusudama3D::get_local_point_in_limits (ik_kusudama_3d.cpp:273-332)
-template <int TA = kTab64>
+template <int TA = kTab64, bool SEL = false>
 __device__ V3 local_point_in_limits(const DevPlan &t, int slot, size_t s, V3 in_point, double &in_bounds) {
 	const int nc = t.cons_ncones[slot];
-	V3 point = normalized(in_point);
+	V3 point = normalized_t<SEL>(in_point);
 	float closest_cos = -2.0f;
 	in_bounds = -1;
 	V3 closest = in_point;
-	const V3 npoint = normalized(point); // closest_to_cone's input.normalized(), the same for every cone
+	const V3 npoint = normalized_t<SEL>(point); // closest_to_cone's input.normalized(), the same for every cone
 	// The first two cones (and the tangent triangle between them) are peeled out of the loops
 	// behind run-time guards: straight-line code for the usual one or two cones, the same
 	// operations in the same order (C2 -1.4 %, C5 -0.4 %, bitwise; profiles/r04_cone_peel_ab.jsonl).
@@ -748,7 +751,7 @@ __device__ V3 local_point_in_limits(const DevPlan &t, int slot, size_t s, V3 in_
 		auto f = [&](int k) { return soa<TA>(t, t.CF, slot, t.cf_stride, o + k, s); };
 		V3 ncp = v3(f(mbik::CFC_NCP), f(mbik::CFC_NCP + 1), f(mbik::CFC_NCP + 2));
 		double rcos = soad<TA>(t, t.CD, slot, t.cd_stride, mbik::CD_PER_CONE * i, s);
-		V3 c = closest_to_cone(ncp, f(mbik::CFC_SR), f(mbik::CFC_CR), rcos, npoint, in_bounds);
+		V3 c = closest_to_cone<SEL>(ncp, f(mbik::CFC_SR), f(mbik::CFC_CR), rcos, npoint, in_bounds);
 		if (is_nan3(c)) {
 			in_bounds = 1;
 			return true;
@@ -772,7 +775,7 @@ __device__ V3 local_point_in_limits(const DevPlan &t, int slot, size_t s, V3 in_
 			auto f = [&](int k) { return soa<TA>(t, t.CF, slot, t.cf_stride, k, s); };
 			auto f3 = [&](int k) { return v3(f(o + k), f(o + k + 1), f(o + k + 2)); };
 			double trcos = soad<TA>(t, t.CD, slot, t.cd_stride, mbik::CD_PER_CONE * i + 1, s);
-			V3 c = great_tangent_triangle(f3(mbik::CFC_C1XC2), f3(mbik::CFC_A1), f3(mbik::CFC_A2), f3(mbik::CFC_B1),
+			V3 c = great_tangent_triangle<SEL>(f3(mbik::CFC_C1XC2), f3(mbik::CFC_A1), f3(mbik::CFC_A2), f3(mbik::CFC_B1),
 					f3(mbik::CFC_B2), f3(mbik::CFC_T1), f3(mbik::CFC_T2), f(o + mbik::CFC_ST), f(o + mbik::CFC_CT), trcos, point);
 			if (isnan(c.x)) return false;
 			float this_cos = dot(c, point);
@@ -1013,7 +1016,8 @@ __device__ __forceinline__ void qcp_accumulate(QSums &S, const V3 wc1, const V3 
 // HELP: the parent-side values come from the helper wave's record hrec (kHelpF4 float4 at
 // stride 64), not from this wave.  XS: the build serves split-exchange tasks (xs, staging 4 /
 // 5): only the two-waves-per-SIMD build, so that the one-wave kernels keep their registers.
-template <bool STAB, bool PR, int TA, bool HELP, bool XS, int PM, class LV, class GV, class FP, class IP>
+// SEL: the orthonormalizations' zero-vector tests as selects (normalized_sel; the one-wave builds).
+template <bool STAB, bool PR, int TA, bool HELP, bool XS, int PM, bool SEL, class LV, class GV, class FP, class IP>
 __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, int xs, size_t s, const LV &L, const GV &G, const FP TG,
 		const FP ST, const IP SF, const FP HS, const FP OE, const FP MS, double &prev_dev, const EffPre &pre, bool hoist,
 		const float4 *hrec, int *hfl, int hseq, bool *hstuck MBIK_PROF_PARAM) {
@@ -1083,7 +1087,7 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, int xs
 			tgt = tgt + tc * -1.0f;
 			translation = tc - mc;
 		}
-		qrot = qcp_single(mvd, tgt);
+		qrot = qcp_single<SEL>(mvd, tgt);
 	} else if (XS && xs) {
 		// Split-exchange (staging 4 / 5; m >= 2, several effectors): lane j of the group builds
 		// the headings of effectors e0+j, e0+j+m, ... with path sharing along its own sequence
@@ -1407,7 +1411,7 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, int xs
 	MBIK_PROF_ADD(1, pt0, pt1);
 	// ---- damp clamp, slerp(…, 0), rotate, translate, set_global_pose (:144-154) ----
 	const double chd = t.seg_cos_half_damp[k];
-	B3 rot = (kAblate & ABL_CONVERT) ? from_quat(qrot) : from_quat(clamp_cos_half(get_rotation_quaternion(from_quat(qrot)), chd));
+	B3 rot = (kAblate & ABL_CONVERT) ? from_quat(qrot) : from_quat(clamp_cos_half(get_rotation_quaternion<SEL>(from_quat(qrot)), chd));
 	MBIK_PROF_T(pc0);
 	MBIK_PROF_ADD(11, pt1, pc0);
 	if constexpr (!(kAblate & ABL_SLERP)) rot = slerp_weight0(rot, sto, t.libm);
@@ -1453,10 +1457,10 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, int xs
 		V3 bdx = xform(Gbd_stale, v3(0.0f, 1.0f, 0.0f));
 		V3 tip = xform(X3{Pinv, xform(Pinv, -Gco.o)}, bdx); // Gco.basis == P.basis
 		double in_bounds = 1.0;
-		V3 inl = local_point_in_limits<TA>(t, slot, s, tip, in_bounds);
+		V3 inl = local_point_in_limits<TA, SEL>(t, slot, s, tip, in_bounds);
 		if (in_bounds < 0) {
 			V3 p2 = xform(Gco, inl);
-			Q rect = arc(bdx - Gco.o, p2 - Gco.o);
+			Q rect = arc<SEL>(bdx - Gco.o, p2 - Gco.o);
 			Lb.b = ((Pinv * from_quat(rect)) * P.b) * Lb.b;
 			swung = true;
 		}
@@ -1485,11 +1489,11 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, int xs
 		if (gs_ok && !swung) Gs.b = GsB;
 		else Gs.b = P.b * Lb.b;
 		if constexpr (!HELP) gtci = inverse(gtc);
-		B3 align = orthonormalized(gtci * Gs.b);
+		B3 align = orthonormalized<SEL>(gtci * Gs.b);
 		Q sw, tw;
-		swing_twist_y(get_rotation_quaternion(align), sw, tw);
+		swing_twist_y(get_rotation_quaternion<SEL>(align), sw, tw);
 		tw = clamp_cos_half(tw, (double)half_cos);
-		B3 recomposition = orthonormalized(gtc * from_quat(sw * tw));
+		B3 recomposition = orthonormalized<SEL>(gtc * from_quat(sw * tw));
 		B3 rotation = Pinv * recomposition;
 		twist_changed = !eq(rotation, Lb.b);
 		Lb.b = rotation;
@@ -1609,11 +1613,12 @@ __device__ __forceinline__ void global_pass(const DevPlan &t, int seg, const LV 
 
 // IKBone3D::set_skeleton_bone_pose (ik_bone_3d.cpp:170-179); returns whether the basis was
 // non-finite (and replaced by the identity, :174-176).
+template <bool SEL = false>
 __device__ bool write_pose(const X3 &t, float *out) {
 	B3 b = t.b;
 	const bool bad = !is_finite(b);
 	if (bad) b = bid();
-	Q q = get_rotation_quaternion(b);
+	Q q = get_rotation_quaternion<SEL>(b);
 	V3 sc = get_scale(b);
 	out[0] = q.x; out[1] = q.y; out[2] = q.z; out[3] = q.w;
 	out[4] = t.o.x; out[5] = t.o.y; out[6] = t.o.z;
@@ -1840,7 +1845,7 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 					if (rp) hrec = rp + (size_t)seq * kHelpF4 * 64;
 #endif
 					if (k0 + q < k1)
-						bone_step<false, true, kTab32, true, false, PM>(t, seg, k0 + q, task.y, task.z, task.w & mbik::SCHED_XS, s, L, G, TG, ST,
+						bone_step<false, true, kTab32, true, false, PM, true>(t, seg, k0 + q, task.y, task.z, task.w & mbik::SCHED_XS, s, L, G, TG, ST,
 								SF, HS, OE, MS, prev_dev, pre, hoist, hrec, b_ready ? nullptr : hfl, seq, &stuck MBIK_PROF_ARG);
 					help_post(hfl + 2, seq + 1);
 					slot = slot + 1 == kHelpSlots ? 0 : slot + 1;
@@ -1893,7 +1898,7 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 					}
 				}
 				if (k >= ke) break;
-				bone_step<STAB, HOIST || PL == 2, TA, false, XS, PM>(t, seg, k, task.y, task.z, task.w & mbik::SCHED_XS, s, L, G, TG, ST, SF,
+				bone_step<STAB, HOIST || PL == 2, TA, false, XS, PM, HOIST>(t, seg, k, task.y, task.z, task.w & mbik::SCHED_XS, s, L, G, TG, ST, SF,
 						HS, OE, MS, prev_dev, pre, hoist, nullptr, nullptr, 0, nullptr MBIK_PROF_ARG);
 				k++;
 			}
@@ -1908,7 +1913,7 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 			float *dst = pose_out + ((size_t)local * B + b) * 10;
 			if (t.bone_flags[b] & mbik::BF_IN_LIST) {
 				if (help_stuck) bad = write_help_timeout(dst);
-				else bad |= write_pose(L.ld(b), dst);
+				else bad |= write_pose<HOIST>(L.ld(b), dst);
 			} else {
 				const float *src = pose_in + ((size_t)local * B + b) * 10;
 				for (int f = 0; f < 10; f++) dst[f] = src[f];
