@@ -1211,7 +1211,7 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, int xs
 		const V3 nmc = mc * -1.0f, ntc = tc * -1.0f;
 		PathCk pc;
 		pc.d = -1;
-		for (int i = e0; i < e1; i++) {
+		auto one = [&](int i, auto tr) __attribute__((always_inline)) {
 			MBIK_PROF_T(ph1);
 			if (hoist) effector_headings<PM>(t, pre, d0, Gb, L, ST, SF, H, OE, oe_mode);
 			else effector_headings<TA, PM>(t, t.seg_effs[i], d0, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, oe_mode,
@@ -1222,13 +1222,48 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, int xs
 			for (int h = 0; h < 7; h++) {
 				if (H.mask & (1 << h)) {
 					const double w = H.w[h];
-					V3 c1 = translate ? H.ht[h] + ntc : H.ht[h];
-					V3 c2 = translate ? H.hm[h] + nmc : H.hm[h];
-					qcp_accumulate(S, c1 * (float)w, c1, c2, w);
+					if constexpr (decltype(tr)::value) {
+						const V3 c1 = H.ht[h] + ntc, c2 = H.hm[h] + nmc;
+						qcp_accumulate(S, c1 * (float)w, c1, c2, w);
+					} else {
+						qcp_accumulate(S, H.ht[h] * (float)w, H.ht[h], H.hm[h], w);
+					}
 				}
 			}
 			MBIK_PROF_T(ph6);
 			MBIK_PROF_ADD(14, ph2, ph6);
+		};
+		// Builds with the state in LDS or the locals in device memory: the translate test taken
+		// out of the heading loop and the first effector peeled (C2 -0.7 %, C3 -1.3 %); the
+		// all-state-in-device-memory build keeps the plain loop (C4 / C5 +0.7 % otherwise;
+		// profiles/r04_one_lane_loop_ab.jsonl).
+		if constexpr (!std::is_same_v<FP, BPtr<float>>) {
+			if (translate) {
+				for (int i = e0; i < e1; i++) one(i, std::true_type{});
+			} else {
+				if (e0 < e1) one(e0, std::false_type{});
+				for (int i = e0 + 1; i < e1; i++) one(i, std::false_type{});
+			}
+		} else {
+			for (int i = e0; i < e1; i++) {
+				MBIK_PROF_T(ph1);
+				if (hoist) effector_headings<PM>(t, pre, d0, Gb, L, ST, SF, H, OE, oe_mode);
+				else effector_headings<TA, PM>(t, t.seg_effs[i], d0, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, OE, oe_mode,
+						PR ? &pc : nullptr, t.seg_eff_lcp + i);
+				MBIK_PROF_T(ph2);
+				MBIK_PROF_ADD(9, ph1, ph2);
+#pragma unroll
+				for (int h = 0; h < 7; h++) {
+					if (H.mask & (1 << h)) {
+						const double w = H.w[h];
+						V3 c1 = translate ? H.ht[h] + ntc : H.ht[h];
+						V3 c2 = translate ? H.hm[h] + nmc : H.hm[h];
+						qcp_accumulate(S, c1 * (float)w, c1, c2, w);
+					}
+				}
+				MBIK_PROF_T(ph6);
+				MBIK_PROF_ADD(14, ph2, ph6);
+			}
 		}
 		MBIK_PROF_T(ph7);
 		qrot = qcp_adjugate(S);
