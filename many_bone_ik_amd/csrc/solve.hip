@@ -586,6 +586,18 @@ __device__ __forceinline__ void effector_headings(const DevPlan &t, const EffPre
 			if (a > b) return;
 			X3 L0 = L.ld(t.eff_path[off + a]);
 			int d = a;
+			// locals in LDS (placement 0): the first trip peeled out of the loop (C2 -1.1 %; the
+			// device-memory placements keep the plain loop, +0.3 % there;
+			// profiles/r04_walk_peel_ab.jsonl)
+			if constexpr (std::is_same_v<LV, LocContig>) {
+				if (d < b) {
+					const X3 L1 = L.ld(t.eff_path[off + d + 1]);
+					X = X * L0;
+					L0 = L.ld(t.eff_path[off + min(d + 2, b)]);
+					X = X * L1;
+					d += 2;
+				}
+			}
 			for (; d < b; d += 2) {
 				const X3 L1 = L.ld(t.eff_path[off + d + 1]);
 				X = X * L0;
