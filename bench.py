@@ -57,7 +57,7 @@ def parse():
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-autotune", action="store_true", help="keep the plan's automatic launch layout")
     ap.add_argument("--layout", default="",
-                    help="pin a launch layout instead of autotuning: K:spw:interval:staging:placement:waves[:helper] "
+                    help="pin a launch layout instead of autotuning: K:spw:interval:staging:placement:waves[:helper[:wave_roles]] "
                          "(mbik_plan_info's fields; tools/round_profile.sh passes the one its first run picked)")
     ap.add_argument("--constraint-mode", action="store_true",
                     help="ManyBoneIK3D::constraint_mode (snaps only; each step is one frame of the persistent node caches)")
@@ -180,6 +180,7 @@ def main():
         fields = [int(x) for x in args.layout.split(":")]
         k, spw, interval, staging, placement, waves = fields[:6]
         plan.set_helper_wave(fields[6] if len(fields) > 6 else 0)
+        plan.set_wave_roles(fields[7] if len(fields) > 7 else 0)
         plan.set_layout(k, spw, interval)
         plan.set_heading_staging(staging)
         plan.set_locals_placement(placement)
@@ -328,7 +329,7 @@ def main():
                    "lanes_per_skeleton": info["lanes_per_skeleton"], "skeletons_per_block": info["skeletons_per_block"],
                    "lds_bytes_per_block": info["lds_bytes_per_block"],
                    "layout": {k: info[k] for k in ("checkpoint_interval", "heading_staging", "state_placement",
-                                                   "waves_per_simd", "helper_wave")},
+                                                   "waves_per_simd", "helper_wave", "wave_roles")},
                    "parallelism": f"dp{world} (skeleton shards, no data-path collective)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_key": tkey,
@@ -363,7 +364,7 @@ def layout_key(info: dict) -> str:
     """The launch layout a plan runs (mbik_plan_info), as the suffix of profiles/traffic.json keys."""
     return (f"K{info['lanes_per_skeleton']}_s{info['skeletons_per_block']}_i{info['checkpoint_interval']}"
             f"_st{info['heading_staging']}_pl{info['state_placement']}_w{info['waves_per_simd']}"
-            + ("_h1" if info.get("helper_wave") else ""))
+            + ("_h1" if info.get("helper_wave") else "") + ("_rw" if info.get("wave_roles") else ""))
 
 
 def timed_gathers(pose_out, total: int, dist, sync, dev) -> dict:

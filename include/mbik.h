@@ -50,7 +50,7 @@ extern "C" {
 #define MBIK_EUNSUPPORTED (-4)
 #define MBIK_ENODEV (-5)
 
-#define MBIK_ABI_VERSION 7
+#define MBIK_ABI_VERSION 8
 
 typedef struct mbik_plan mbik_plan;
 typedef struct mbik_group mbik_group;
@@ -119,6 +119,9 @@ typedef struct mbik_plan_info {
 	                                      priorities differ, and each effector's slots are tested at run
 	                                      time (ABI 7).  Bits: 0 the origin heading, 1+2a and 2+2a the
 	                                      +/- headings of axis a. */
+	int32_t wave_roles;                /* 1 when the current layout runs with wave roles
+	                                      (mbik_plan_set_wave_roles): lanes_per_skeleton is then the
+	                                      number of waves per block (ABI 8) */
 } mbik_plan_info;
 
 /* Which reference host the plan reproduces bit for bit (ABI 4).  Godot's Math::sin/cos(float)
@@ -157,7 +160,7 @@ void mbik_plan_destroy(mbik_plan *plan);
  * buf == NULL stores the needed size in *size; otherwise capacity must be at least that
  * (MBIK_EINVAL).  It reads the device tables back, so the streams using the plan must be
  * idle.  mbik_plan_load rebuilds the plan on `device` from such a buffer; the loaded plan
- * solves bitwise like the saved one.  Format version 4 (1-3 still load), little-endian,
+ * solves bitwise like the saved one.  Format version 5 (1-4 still load), little-endian,
  * host-independent. */
 int32_t mbik_plan_save(const mbik_plan *plan, void *buf, uint64_t capacity, uint64_t *size);
 int32_t mbik_plan_load(const void *buf, uint64_t size, int32_t device, mbik_plan **out_plan);
@@ -217,6 +220,17 @@ int32_t mbik_plan_set_waves_per_simd(mbik_plan *plan, int32_t waves);
  * return MBIK_EHIP, without launching, on the plan's next call, which clears the flag.
  * Plans never see each other's timeouts. */
 int32_t mbik_plan_set_helper_wave(mbik_plan *plan, int32_t helper);
+/* Wave roles (ABI 8): one wavefront per segment, a lane per skeleton.  A block is 64 skeletons
+ * and K waves; the K roles of the sibling-segment schedule (lanes_per_skeleton, a power of two
+ * 2..8; 8 only with two waves per SIMD) are the block's waves instead of K lanes of one wave, so
+ * sibling segments run on separate waves that meet at a barrier per tree level, each wave reads
+ * its segment's topology as wave-uniform values, and no lane repeats another lane's work (a
+ * segment with fewer lanes than effectors is solved by one wave, effector by effector, in the
+ * reference's order: ik_bone_segment_3d.cpp:210-240).  The whole solve state lives in device
+ * memory (state placement 2).  1 on, 0 off, -1 (default) automatic: off until mbik_plan_autotune
+ * has timed it.  Plans with stabilization passes, constraint_mode plans and plans whose setup
+ * tables need 64-bit indices run without it.  Results do not depend on it. */
+int32_t mbik_plan_set_wave_roles(mbik_plan *plan, int32_t roles);
 /* Status of a plan's earlier launches, for callers that poll instead of waiting for the next
  * call's return code (ABI 6): *status = MBIK_STATUS_HELPER_TIMEOUT when a helper-wave launch of
  * this plan that has completed timed out (see mbik_plan_set_helper_wave), else 0.  Reading

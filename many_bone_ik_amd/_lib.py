@@ -29,7 +29,7 @@ GLIBC_SSE2_TUNABLES = "glibc.cpu.hwcaps=-FMA,-AVX2_Usable"
 EXPORTED_SYMBOLS = (
     "mbik_plan_create", "mbik_plan_create_opts", "mbik_plan_create_device_opts", "mbik_plan_destroy", "mbik_plan_save", "mbik_plan_load", "mbik_plan_get_info", "mbik_plan_set_launch", "mbik_plan_set_layout",
     "mbik_plan_autotune", "mbik_plan_resident_blocks", "mbik_plan_set_heading_staging",
-    "mbik_plan_set_locals_placement", "mbik_plan_set_waves_per_simd", "mbik_plan_set_helper_wave", "mbik_plan_set_table_addressing", "mbik_plan_rebuild_setup", "mbik_plan_setup_tables",
+    "mbik_plan_set_locals_placement", "mbik_plan_set_waves_per_simd", "mbik_plan_set_helper_wave", "mbik_plan_set_wave_roles", "mbik_plan_set_table_addressing", "mbik_plan_rebuild_setup", "mbik_plan_setup_tables",
     "mbik_plan_status", "mbik_plan_debug_helper",
     "mbik_solve", "mbik_solve_checked", "mbik_solve_host", "mbik_segment_solve", "mbik_plan_segment_table", "mbik_describe_topology",
     "mbik_group_create", "mbik_group_solve", "mbik_group_destroy", "mbik_capture_targets", "mbik_selftest_math",
@@ -69,7 +69,7 @@ class MbikPlanInfo(C.Structure):
                 ("checkpoint_interval", C.c_int32), ("heading_staging", C.c_int32), ("state_placement", C.c_int32),
                 ("waves_per_simd", C.c_int32), ("constraint_slots", C.c_int32), ("cf_stride", C.c_int32),
                 ("cd_stride", C.c_int32), ("libm_variant", C.c_int32),
-                ("helper_wave", C.c_int32), ("heading_slots", C.c_int32)]
+                ("helper_wave", C.c_int32), ("heading_slots", C.c_int32), ("wave_roles", C.c_int32)]
 
 
 class MbikPlanOptions(C.Structure):
@@ -132,6 +132,9 @@ def load():
     if hasattr(L, "mbik_plan_set_helper_wave"):  # (absent from older A/B builds)
         L.mbik_plan_set_helper_wave.argtypes = [vp, C.c_int32]
         L.mbik_plan_set_helper_wave.restype = C.c_int32
+    if hasattr(L, "mbik_plan_set_wave_roles"):  # (ABI 8; absent from older A/B builds)
+        L.mbik_plan_set_wave_roles.argtypes = [vp, C.c_int32]
+        L.mbik_plan_set_wave_roles.restype = C.c_int32
     if hasattr(L, "mbik_plan_status"):  # (ABI 6; absent from older A/B builds)
         L.mbik_plan_status.argtypes = [vp, C.POINTER(C.c_uint32)]
         L.mbik_plan_status.restype = C.c_int32

@@ -668,6 +668,15 @@ void build_schedule(HostPlan &p, int32_t lanes, int64_t nlaunch, int32_t spw_ove
 		for (size_t start = 0; start < l.size(); start += K) {
 			int cnt = (int)std::min<size_t>(K, l.size() - start);
 			int m = K >> ceil_log2(cnt);
+			if (p.wave_roles) {
+				// Wave roles: one wave per segment (no group of lanes repeating its work); the
+				// row's segments spread over the block's waves, the others wait at the row barrier.
+				std::vector<SchedTask> row(K, SchedTask{-1, 0, 1, 0});
+				for (int i = 0; i < cnt; i++) row[i * m] = SchedTask{l[start + i], 0, 1, 0};
+				p.sched.insert(p.sched.end(), row.begin(), row.end());
+				p.nrows++;
+				continue;
+			}
 			// without staging, the m lanes of a group each solve the whole segment (j 0 of 1):
 			// identical work and identical stores, so no lane waits on another
 			std::vector<SchedTask> row(K, SchedTask{-1, 0, 1, 0});
@@ -763,7 +772,11 @@ void build_schedule(HostPlan &p, int32_t lanes, int64_t nlaunch, int32_t spw_ove
 	int best = 64 / K;
 	while (best > 1 && resident(best) == 0) best--;
 	int best_c = interval_override > 0 ? interval_override : 1;
-	if (spw_override > 0) {
+	if (p.wave_roles) {
+		// wave roles: a lane per skeleton, 64 per block of K waves; the state is in device
+		// memory, so LDS holds the topology and the block's 64 non-finite flags only
+		best = 64;
+	} else if (spw_override > 0) {
 		best = std::min(spw_override, 64 / K);
 		while (best > 1 && resident(best) == 0) best--;
 	} else if (resident(best) * kCUs < nlaunch) {
@@ -800,7 +813,7 @@ void build_schedule(HostPlan &p, int32_t lanes, int64_t nlaunch, int32_t spw_ove
 		r[3] = c0 | ((c1 - c0) << 16);
 	}
 	p.spw = best;
-	p.lds_block_bytes = best * (int64_t)(((lds_floats_per_skeleton(p) + 3) & ~3) * 4) + topo;
+	p.lds_block_bytes = best * (int64_t)(((lds_floats_per_skeleton(p) + 3) & ~3) * 4) + topo + (p.wave_roles ? 64 * 4 : 0);
 }
 
 } // namespace mbik

@@ -123,6 +123,11 @@ struct HostPlan {
 	int32_t state_hbm = 0;
 	// Waves per SIMD the solve kernel's registers are sized for (1, or 2 with spills).
 	int32_t waves_per_simd = 1;
+	// Wave roles (the north star's "one wavefront per segment"): each lane of a wave is one
+	// skeleton (64 per block) and the K roles of the sibling schedule are the block's K waves, so a
+	// segment runs on one wave with its topology wave-uniform and no lane of a skeleton repeats
+	// another's work.  Whole state in device memory (state_hbm 2).  0: roles are lanes of a wave.
+	int32_t wave_roles = 0;
 	// Iteration-start globals kept in LDS only for checkpoint bones: every g_interval-th bone
 	// of a segment counted from its root (the root included) and every parent of a segment
 	// root; a bone-step rebuilds its parent's global from the nearest checkpoint above it.

@@ -862,9 +862,15 @@ __device__ __forceinline__ void help_give_up(int *hfl, bool &stuck) {
 	stuck = true;
 	__hip_atomic_store(hfl + HC_STUCK, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-__device__ __forceinline__ bool help_expired(uint64_t &t0, int &seen, int now_val, uint64_t timeout) {
+// t0: when the counter was last seen to move; tl: the previous poll.  Polls come every s_sleep
+// (microseconds apart), so a gap between two polls of more than timeout / 200 (10 ms of the 2 s
+// deadline) means the waves were suspended (preemption, context save/restore), not that the
+// partner stalled: the deadline restarts instead of counting the gap.
+__device__ __forceinline__ bool help_expired(uint64_t &t0, uint64_t &tl, int &seen, int now_val, uint64_t timeout) {
 	const uint64_t now = (uint64_t)wall_clock64();
-	if (t0 == 0 || now_val != seen) {
+	const bool resumed = t0 != 0 && now - tl > timeout / 200;
+	tl = now;
+	if (t0 == 0 || now_val != seen || resumed) {
 		t0 = now;
 		seen = now_val;
 		return false;
@@ -873,12 +879,12 @@ __device__ __forceinline__ bool help_expired(uint64_t &t0, int &seen, int now_va
 }
 __device__ __forceinline__ void help_wait(int *hfl, int k, int v, bool &stuck, uint64_t timeout) {
 	if (stuck) return;
-	uint64_t t0 = 0;
+	uint64_t t0 = 0, tl = 0;
 	int seen = 0;
 	for (;;) {
 		const int c = __builtin_amdgcn_readfirstlane(__hip_atomic_load(hfl + k, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
 		if (c >= v) return;
-		if (help_expired(t0, seen, c, timeout)) return help_give_up(hfl, stuck);
+		if (help_expired(t0, tl, seen, c, timeout)) return help_give_up(hfl, stuck);
 		__builtin_amdgcn_s_sleep(1);
 	}
 }
@@ -888,7 +894,7 @@ __device__ __forceinline__ void help_wait_ab(int *hfl, int v, bool &stuck, bool 
 	b_ready = stuck;
 	if (stuck) return;
 	unsigned long long *f2 = reinterpret_cast<unsigned long long *>(hfl);
-	uint64_t t0 = 0;
+	uint64_t t0 = 0, tl = 0;
 	int seen = 0;
 	for (;;) {
 		const unsigned long long ab = __hip_atomic_load(f2, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -897,7 +903,7 @@ __device__ __forceinline__ void help_wait_ab(int *hfl, int v, bool &stuck, bool 
 			b_ready = b >= v;
 			return;
 		}
-		if (help_expired(t0, seen, a, timeout)) {
+		if (help_expired(t0, tl, seen, a, timeout)) {
 			b_ready = true;
 			return help_give_up(hfl, stuck);
 		}
@@ -1716,13 +1722,16 @@ __device__ __forceinline__ int row_steps(const DevPlan &t, int r, int seg_lo, in
 	return __builtin_amdgcn_readfirstlane(n);
 }
 
-template <bool STAB, int PL, bool HOIST = true, bool T32 = true, bool HELP = false, bool XS = false, int PM = 0>
+// RW (wave roles, HostPlan::wave_roles): the block is RW waves; lane = skeleton (64 per block),
+// wave = the schedule's role, so every topology value a wave reads is uniform over it.
+template <bool STAB, int PL, bool HOIST = true, bool T32 = true, bool HELP = false, bool XS = false, int PM = 0, int RW = 0>
 __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int count, const float *__restrict__ pose_in,
 		const float *__restrict__ targets, float *__restrict__ pose_out, int iterations, int seg_lo, int seg_hi) {
 	static_assert(!HELP || (!STAB && PL == 0), "the helper wave serves placement-0 launches without stabilization");
+	static_assert(!RW || (!STAB && !HELP && !XS && PL == 2), "wave roles: whole state in device memory, no stabilization");
 	extern __shared__ float4 lds4[];
-	const int lane = HELP ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
-	const int wave = HELP ? (int)(threadIdx.x >> 6) : 0;
+	const int lane = (HELP || RW) ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
+	const int wave = HELP ? (int)(threadIdx.x >> 6) : RW ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;
 #ifdef MBIK_PROF
 	uint64_t pfa[24] = {};
 	uint64_t *pf = pfa;
@@ -1730,7 +1739,7 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 	MBIK_PROF_T(pk0);
 	{
 		uint4 *dst = reinterpret_cast<uint4 *>(lds4);
-		for (int i = (int)threadIdx.x; i < (t.topo_words >> 2); i += HELP ? 128 : 64) dst[i] = t.topo_blob[i];
+		for (int i = (int)threadIdx.x; i < (t.topo_words >> 2); i += HELP ? 128 : RW ? 64 * RW : 64) dst[i] = t.topo_blob[i];
 	}
 	const uint32_t *topo = reinterpret_cast<const uint32_t *>(lds4);
 #define MBIK_REPOINT(T, name) t.name = reinterpret_cast<const T *>(topo + t.o_##name);
@@ -1746,12 +1755,12 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 		for (int i = lane; i < t.NC * t.cd_stride; i += 64) xl[i] = t.CD[(size_t)i * t.N + first];
 		t.D = dl; t.CF = cl; t.CD = xl; t.N = 1;
 	}
-	const int g = lane >> t.log2K;
-	const int role = lane & (t.K - 1);
+	const int g = RW ? lane : lane >> t.log2K;
+	const int role = RW ? wave : lane & (t.K - 1);
 	const int local = blk * t.spw + g;
 	const bool valid = g < t.spw && local < count;
 	const size_t s = (size_t)first + (size_t)(valid ? local : 0);
-	const int B = t.B, P = t.P, K = t.K;
+	const int B = t.B, P = t.P, K = RW ? RW : t.K;
 	// PL (HostPlan::state_hbm): 0 the state in LDS; 1 the locals in device memory (L2-resident
 	// during the launch), the rest in LDS; 2 all of it in device memory
 	// FP / IP: the float / int state pointers: LDS, or for PL 2 BPtr into device memory.  (PL 1
@@ -1787,7 +1796,12 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 	constexpr int TA = PL == 2 ? kTabTiled : (T32 ? kTab32 : kTab64); // placement 2 reads the tiled table copy
 	const FP OE = rebind<float>(uplus(SF, P));    // stabilization only: 3 per pin
 	const FP MS = uplus(OE, 3 * P);              // stabilization only: 7 per pin
-	if (valid && wave == 0) {
+	// wave roles: the block's 64 non-finite flags, after the topology (write_nonfinite)
+	int *nf_rw = RW ? reinterpret_cast<int *>(lds) : nullptr;
+	if constexpr (RW) {
+		if (threadIdx.x < 64) nf_rw[threadIdx.x] = 0;
+	}
+	if (valid && (RW || wave == 0)) {
 		for (int b = role; b < B; b += K)
 			if (t.bone_flags[b] & mbik::BF_IN_LIST) L.st(b, pose_to_xform(pose_in + ((size_t)local * B + b) * 10));
 		for (int e = role; e < P; e += K) {
@@ -1973,7 +1987,14 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 			}
 		}
 	}
-	write_nonfinite(t, valid, bad, g, role, local);
+	if constexpr (RW) {
+		// a skeleton's bones are written by all K waves: their flags meet in LDS
+		if (valid && bad) nf_rw[lane] = 1;
+		__syncthreads();
+		if (t.nonfinite && valid && wave == 0) t.nonfinite[local] = nf_rw[lane] != 0;
+	} else {
+		write_nonfinite(t, valid, bad, g, role, local);
+	}
 	if (help_stuck && lane == 0 && t.help_flag) __hip_atomic_store(t.help_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 	MBIK_PROF_T(pk3);
 	MBIK_PROF_ADD(6, pk2, pk3);
@@ -2009,6 +2030,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) 
 
 // The same with a helper wave (two waves per block, on two SIMDs of a CU): placement 0, no
 // stabilization, 32-bit table addressing (mbik_plan_set_helper_wave; autotune decides).
+// Wave roles (HostPlan::wave_roles): KW waves per block, one per role of the sibling schedule,
+// a lane per skeleton; the whole state in device memory.  WPE as above: KW waves of a block
+// need KW / 4 waves per SIMD.
+template <int KW, int WPE, int PM>
+__global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void mbik_solve_kernel_rw(DevPlan t, int first,
+		int count, const float *__restrict__ pose_in, const float *__restrict__ targets, float *__restrict__ pose_out, int iterations,
+		int seg_lo, int seg_hi) {
+	static_assert(KW <= 4 * WPE, "a block's waves must fit the CU at this register budget");
+	solve_block<false, 2, WPE == 1, true, false, false, PM, KW>(t, xcd_block(), first, count, pose_in, targets, pose_out, iterations,
+			seg_lo, seg_hi);
+}
+
 template <int PM>
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(1, 1))) void mbik_solve_kernel_help(DevPlan t, int first, int count,
 		const float *__restrict__ pose_in, const float *__restrict__ targets, float *__restrict__ pose_out, int iterations, int seg_lo,
@@ -2142,7 +2175,8 @@ struct mbik_plan {
 	int locals_override = -1;                            // mbik_plan_set_locals_placement; -1 = automatic
 	int waves_override = -1;                             // mbik_plan_set_waves_per_simd; -1 = automatic
 	int helper_override = -1;                            // mbik_plan_set_helper_wave; -1 = automatic
-	int sched_locals = -1;
+	int roles_override = -1;                             // mbik_plan_set_wave_roles; -1 = automatic (off until autotuned)
+	int sched_locals = -1, sched_roles = -1;
 	float *d_locals = nullptr;                           // [N][B][12] for state_hbm 1
 	float *d_state = nullptr;                            // [N][state stride] for state_hbm 2
 	size_t d_state_floats = 0;
@@ -2288,13 +2322,25 @@ SolveKernel solve_kernel_for(const mbik_plan *p) {
 			mbik_solve_kernel<false, 2, 2, true, false, D>};
 	static const SolveKernel k2xd[3] = {mbik_solve_kernel<false, 0, 2, true, true, D>, mbik_solve_kernel<false, 1, 2, true, true, D>,
 			mbik_solve_kernel<false, 2, 2, true, true, D>};
+	// wave roles: [PM default?][K 2 / 4 / 8, waves per SIMD 1 / 2] (K 8 needs two waves per SIMD)
+	static const SolveKernel krw[2][5] = {
+			{mbik_solve_kernel_rw<2, 1, 0>, mbik_solve_kernel_rw<2, 2, 0>, mbik_solve_kernel_rw<4, 1, 0>, mbik_solve_kernel_rw<4, 2, 0>,
+					mbik_solve_kernel_rw<8, 2, 0>},
+			{mbik_solve_kernel_rw<2, 1, D>, mbik_solve_kernel_rw<2, 2, D>, mbik_solve_kernel_rw<4, 1, D>, mbik_solve_kernel_rw<4, 2, D>,
+					mbik_solve_kernel_rw<8, 2, D>}};
 	static std::once_flag once;
 	std::call_once(once, [] {
 		for (auto &row : ks)
 			for (SolveKernel k : row) (void)hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 		for (const SolveKernel *a : {k2, k2x, k64, kd, k2d, k2xd})
 			for (int i = 0; i < 3; i++) (void)hipFuncSetAttribute((const void *)a[i], hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+		for (auto &row : krw)
+			for (SolveKernel k : row) (void)hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 	});
+	if (h.wave_roles) {
+		const int i = h.K == 2 ? (h.waves_per_simd == 2 ? 1 : 0) : h.K == 4 ? (h.waves_per_simd == 2 ? 3 : 2) : 4;
+		return krw[p->dev.prio_mask == kPrioDefault ? 1 : 0][i];
+	}
 	const int pl = std::min(2, std::max(0, (int)h.state_hbm));
 	const bool two = h.waves_per_simd == 2 && h.stabilization_passes == 0;
 	if (pl == 0 && !tables_fit_32(p)) return two ? k64[2] : k64[h.stabilization_passes > 0 ? 1 : 0];
@@ -2342,8 +2388,9 @@ int ensure_help_flag(mbik_plan *p) {
 // written as failures (write_help_timeout) and flagged non-finite.  The asynchronous calls report
 // it on the plan's next call; the synchronous ones right after their own launch.
 int take_helper_timeout(mbik_plan *p) {
-	if (!p->help_flag || __atomic_load_n(p->help_flag, __ATOMIC_ACQUIRE) == 0u) return MBIK_OK;
-	__atomic_store_n(p->help_flag, 0u, __ATOMIC_RELEASE);
+	// one exchange: a still-running launch that sets the flag between a load and a clear would
+	// otherwise have its timeout cleared unreported
+	if (!p->help_flag || __atomic_exchange_n(p->help_flag, 0u, __ATOMIC_ACQ_REL) == 0u) return MBIK_OK;
 	return fail(MBIK_EHIP, "helper wave: a launch of this plan timed out in the two-wave handshake; its skeletons "
 						   "were written as failures (identity rotation, NaN position) and flagged non-finite");
 }
@@ -2370,6 +2417,25 @@ int ensure_schedule(mbik_plan *p, int64_t nlaunch) {
 	h.staging = p->staging_override < 0 ? 1 : p->staging_override;
 	h.state_hbm = h.constraint_mode ? 0 : std::max(0, p->locals_override);
 	h.waves_per_simd = (p->waves_override == 2 && !h.constraint_mode && h.stabilization_passes == 0) ? 2 : 1;
+	// Wave roles (mbik_plan_set_wave_roles): the whole state in device memory, one wave per role
+	// (K = 2, 4 or 8 waves per block; 8 only at two waves per SIMD), no stabilization, 32-bit tables.
+	h.wave_roles = p->roles_override == 1 && !h.constraint_mode && h.stabilization_passes == 0 && tables_fit_32(p) ? 1 : 0;
+	if (h.wave_roles) {
+		const int cap = 4 * h.waves_per_simd;
+		int roles = std::min(lanes, cap);
+		if (roles == 0) {
+			mbik::build_schedule(h, 0, nlaunch, 0, p->interval_override, nullptr, nullptr, p->cu_count);
+			roles = std::min(h.K, cap);
+		}
+		// one role is the classic layout with 64 skeletons per wave: no wave roles then
+		if (roles >= 2) {
+			lanes = roles;
+			h.state_hbm = 2;
+			h.staging = 0;
+		} else {
+			h.wave_roles = 0;
+		}
+	}
 	if (h.state_hbm >= 1 && !tables_fit_32(p))
 		return fail(MBIK_EUNSUPPORTED, "state placements 1 and 2 need every setup table < 4 GiB (fewer skeletons per plan)");
 	if (h.state_hbm >= 1 && !p->d_locals) {
@@ -2428,7 +2494,7 @@ int ensure_schedule(mbik_plan *p, int64_t nlaunch) {
 		p->dev.state_stride = stride;
 	}
 	if (p->sched_K == h.K && p->sched_c == h.g_interval && p->sched_staging == h.staging &&
-			p->sched_locals == h.state_hbm && p->d_sched) {
+			p->sched_locals == h.state_hbm && p->sched_roles == h.wave_roles && p->d_sched) {
 		p->dev.spw = h.spw;
 		return MBIK_OK;
 	}
@@ -2438,6 +2504,7 @@ int ensure_schedule(mbik_plan *p, int64_t nlaunch) {
 	p->sched_c = h.g_interval;
 	p->sched_staging = h.staging;
 	p->sched_locals = h.state_hbm;
+	p->sched_roles = h.wave_roles;
 	p->dev.nrows = h.nrows;
 	p->dev.K = h.K;
 	p->dev.log2K = h.log2K;
@@ -2678,7 +2745,10 @@ int launch(mbik_plan *p, int first, int count, const float *pose_in, const float
 	unsigned blocks = (unsigned)((count + h.spw - 1) / h.spw);
 	auto kern = solve_kernel_for(p);
 	unsigned threads = 64;
-	if (helper_on(p)) {
+	if (h.wave_roles) {
+		threads = 64u * (unsigned)h.K; // a wave per role
+		lds += 64 * sizeof(int);      // the block's non-finite flags
+	} else if (helper_on(p)) {
 		static std::once_flag honce;
 		std::call_once(honce, [] {
 			(void)hipFuncSetAttribute((const void *)mbik_solve_kernel_help<0>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -3136,7 +3206,7 @@ int32_t mbik_plan_create_device_opts(int32_t n_rigs, const mbik_skeleton_desc *d
 // ---- plan serialisation (mbik_plan_save / mbik_plan_load) ----
 namespace {
 constexpr char kPlanMagic[8] = {'M', 'B', 'I', 'K', 'P', 'L', 'A', 'N'};
-constexpr uint32_t kPlanFormat = 4; // 2: + the table-addressing override; 3: + libm_variant, constraint_mode spw; 4: + the helper-wave override (1-3 are still read)
+constexpr uint32_t kPlanFormat = 5; // 2: + the table-addressing override; 3: + libm_variant, constraint_mode spw; 4: + the helper-wave override; 5: + the wave-roles override (1-4 are still read)
 struct PlanWriter {
 	std::vector<char> b;
 	void bytes(const void *v, size_t n) {
@@ -3233,6 +3303,7 @@ int32_t mbik_plan_save(const mbik_plan *p, void *buf, uint64_t capacity, uint64_
 	w.vec(cm);
 	w.put<int32_t>(h.libm_variant); // format 3
 	w.put<int32_t>(p->helper_override); // format 4
+	w.put<int32_t>(p->roles_override); // format 5
 	*size = w.b.size();
 	if (!buf) return MBIK_OK;
 	if (capacity < w.b.size()) return fail(MBIK_EINVAL, "buffer smaller than the saved plan (see *size)");
@@ -3274,9 +3345,11 @@ int32_t mbik_plan_load(const void *buf, uint64_t size, int32_t device, mbik_plan
 	std::vector<char> cm = r.vec<char>(kMax);
 	const int32_t libm = format >= 3 ? r.get<int32_t>() : MBIK_LIBM_VARIANT_FMA;
 	const int32_t helper = format >= 4 ? r.get<int32_t>() : -1;
+	const int32_t roles = format >= 5 ? r.get<int32_t>() : -1;
 	if (!r.ok || N <= 0) return fail(MBIK_EINVAL, "truncated or corrupt saved plan");
 	if (libm != MBIK_LIBM_VARIANT_FMA && libm != MBIK_LIBM_VARIANT_SSE2) return fail(MBIK_EINVAL, "saved plan: unknown libm_variant");
 	if (helper < -1 || helper > 1) return fail(MBIK_EINVAL, "saved plan: unknown helper-wave setting");
+	if (roles < -1 || roles > 1) return fail(MBIK_EINVAL, "saved plan: unknown wave-roles setting");
 	mbik_skeleton_desc desc{};
 	desc.bone_count = (int32_t)p->src_parents.size();
 	desc.parents = p->src_parents.data();
@@ -3313,6 +3386,7 @@ int32_t mbik_plan_load(const void *buf, uint64_t size, int32_t device, mbik_plan
 	p->tab64 = ov[7] != 0;
 	p->cm_spw_div = std::max(0, std::min(6, ov[8]));
 	p->helper_override = helper;
+	p->roles_override = roles;
 	if (h.constraint_mode) {
 		const int W = std::max(1, (h.cm_npos + 31) / 32);
 		const size_t want = (size_t)(3 * h.B + 2 * h.NC) * 12 * n * sizeof(float) + 4 * (size_t)W * n * sizeof(uint32_t);
@@ -3368,6 +3442,7 @@ int32_t mbik_plan_get_info(const mbik_plan *p, mbik_plan_info *o) {
 	o->libm_variant = h.libm_variant;
 	o->helper_wave = helper_on(p) ? 1 : 0;
 	o->heading_slots = p->dev.prio_mask;
+	o->wave_roles = h.wave_roles;
 	return MBIK_OK;
 }
 
@@ -3403,6 +3478,14 @@ int32_t mbik_plan_set_helper_wave(mbik_plan *p, int32_t helper) {
 	if (!p) return fail(MBIK_EINVAL, "null plan");
 	if (helper < -1 || helper > 1) return fail(MBIK_EINVAL, "helper wave must be -1 (automatic), 0 (off) or 1 (on)");
 	p->helper_override = helper;
+	return MBIK_OK;
+}
+
+int32_t mbik_plan_set_wave_roles(mbik_plan *p, int32_t roles) {
+	if (!p) return fail(MBIK_EINVAL, "null plan");
+	if (roles < -1 || roles > 1) return fail(MBIK_EINVAL, "wave roles must be -1 (automatic), 0 (off) or 1 (on)");
+	p->roles_override = roles;
+	p->sched_K = -1;
 	return MBIK_OK;
 }
 
@@ -3621,7 +3704,8 @@ int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const flo
 	const int staging0 = p->staging_override;
 	const int locals0 = p->locals_override;
 	const int waves0 = p->waves_override;
-	{
+	const int roles0 = p->roles_override;
+	if (roles0 != 1) {
 		// A launch whose skeletons are all resident at the default layout is bound by one
 		// skeleton's dependency chain; no layout shortens that, so there is nothing to time.
 		p->spw_override = 0;
@@ -3629,10 +3713,13 @@ int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const flo
 		p->staging_override = staging0 < 0 ? 1 : staging0;
 		p->locals_override = locals0 < 0 ? 0 : locals0;
 		p->waves_override = waves0 < 0 ? 1 : waves0;
+		p->roles_override = 0;
 		int rc0 = ensure_schedule(p, count);
 		if (rc0 != MBIK_OK) return rc0;
-		if ((int64_t)blocks_per_cu(p, p->host.lds_block_bytes) * p->host.spw * p->cu_count >= count && p->host.g_interval == 1)
+		if ((int64_t)blocks_per_cu(p, p->host.lds_block_bytes) * p->host.spw * p->cu_count >= count && p->host.g_interval == 1) {
+			p->roles_override = roles0 < 0 ? 0 : roles0;
 			return autotune_helper(p, first, count, pose_in, targets, pose_out, st);
+		}
 	}
 	// Candidate layouts: for each heading-staging mode and checkpoint interval, the largest
 	// skeletons-per-block at each distinct residency (blocks per CU).  Every layout computes
@@ -3649,7 +3736,24 @@ int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const flo
 	}
 	std::vector<int> lane_cands = {lanes};
 	if (lanes == 0 && p->host.K >= 2) lane_cands.push_back(p->host.K / 2);
-	std::vector<std::tuple<int, int, int, int, int, int>> cands; // (spw override, interval, staging, state placement, lanes, waves)
+	std::vector<std::tuple<int, int, int, int, int, int, int>> cands; // (spw override, interval, staging, state placement, lanes, waves, wave roles)
+	// Wave roles (one wave per role, a lane per skeleton, 64 per block): the widest sibling level
+	// and its halves as the number of waves, within what a CU holds at the register budget.
+	// (after the classic candidates, so that a near-tie keeps the classic layout)
+	std::vector<std::tuple<int, int, int, int, int, int, int>> rw_cands;
+	p->host.wave_roles = 0;
+	if (roles0 != 0 && p->host.stabilization_passes == 0 && !p->host.constraint_mode) {
+		mbik::build_schedule(p->host, 0, count, 0, 0, nullptr, nullptr, p->cu_count);
+		const int widest = p->host.K;
+		for (int wv : {1, 2}) {
+			if (waves0 > 0 && wv != waves0) continue;
+			for (int k : lanes > 0 ? std::vector<int>{lanes} : std::vector<int>{widest, widest / 2, widest / 4}) {
+				if (k < 2 || k > 4 * wv) continue;
+				for (int c : {1, 2}) rw_cands.push_back({0, c, 0, 2, k, wv, 1});
+			}
+		}
+	}
+	if (roles0 != 1)
 	for (int wv : {1, 2}) {
 	if (waves0 > 0 && wv != waves0) continue;
 	if (wv == 2 && p->host.stabilization_passes > 0) continue;
@@ -3685,7 +3789,7 @@ int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const flo
 						if (p->host.spw != spw) continue; // capped by 64 / K or by LDS
 						const int blocks = blocks_per_cu(p, p->host.lds_block_bytes);
 						if (blocks != last_blocks) {
-							cands.push_back({spw, c, stg, lh, ln, wv});
+							cands.push_back({spw, c, stg, lh, ln, wv, 0});
 							last_blocks = blocks;
 						}
 					}
@@ -3695,23 +3799,25 @@ int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const flo
 		}
 	}
 	}
+	cands.insert(cands.end(), rw_cands.begin(), rw_cands.end());
 	hipEvent_t e0, e1;
 	if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return fail(MBIK_EHIP, "hipEventCreate");
 	float best_ms = 0.0f;
-	int best_spw = 0, best_c = 0, best_stg = 1, best_lh = 0, best_ln = lanes, best_wv = 1, rc = MBIK_OK;
-	std::vector<std::tuple<int, int, int, int, int, int>> seen; // resolved (K, spw, interval, staging, locals, waves)
+	int best_spw = 0, best_c = 0, best_stg = 1, best_lh = 0, best_ln = lanes, best_wv = 1, best_rw = 0, rc = MBIK_OK;
+	std::vector<std::tuple<int, int, int, int, int, int, int>> seen; // resolved (K, spw, interval, staging, locals, waves, roles)
 	struct Timed {
 		float ms;
-		int spw, interval, stg, lh, ln, wv;
+		int spw, interval, stg, lh, ln, wv, rw;
 	};
 	std::vector<Timed> timed;
-	for (auto [spw, c, stg, lh, ln, wv] : cands) {
+	for (auto [spw, c, stg, lh, ln, wv, rw] : cands) {
 		p->spw_override = spw;
 		p->interval_override = c;
 		p->lanes_override = ln;
 		p->staging_override = stg;
 		p->locals_override = lh;
 		p->waves_override = wv;
+		p->roles_override = rw;
 		if ((rc = ensure_schedule(p, count)) != MBIK_OK) {
 			// a placement this batch cannot have (device memory, or the 4 GiB buffer limit) is skipped
 			if (rc == MBIK_ENOMEM || rc == MBIK_EUNSUPPORTED) {
@@ -3720,7 +3826,7 @@ int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const flo
 			}
 			break;
 		}
-		const auto key = std::make_tuple(p->host.K, p->host.spw, p->host.g_interval, stg, lh, wv);
+		const auto key = std::make_tuple(p->host.K, p->host.spw, p->host.g_interval, stg, lh, wv, (int)p->host.wave_roles);
 		if (std::find(seen.begin(), seen.end(), key) != seen.end()) continue;
 		seen.push_back(key);
 		if ((rc = launch(p, first, count, pose_in, targets, pose_out, st, p->host.iterations, 0, p->host.NS - 1)) != MBIK_OK) break;
@@ -3735,7 +3841,7 @@ int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const flo
 		}
 		float ms = 0.0f;
 		(void)hipEventElapsedTime(&ms, e0, e1);
-		timed.push_back({ms, p->host.spw, p->host.g_interval, stg, lh, ln, wv});
+		timed.push_back({ms, p->host.spw, p->host.g_interval, stg, lh, ln, wv, rw});
 		if (best_c == 0 || ms < best_ms) {
 			best_ms = ms;
 			best_c = p->host.g_interval;
@@ -3754,8 +3860,10 @@ int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const flo
 			best_lh = c.lh;
 			best_ln = c.ln;
 			best_wv = c.wv;
+			best_rw = c.rw;
 			break;
 		}
+	p->roles_override = best_rw;
 	p->spw_override = best_spw;
 	p->interval_override = best_c;
 	p->staging_override = best_stg;

@@ -232,6 +232,11 @@ class Plan:
         -1 automatic."""
         check(self._L.mbik_plan_set_helper_wave(self.h, int(helper)))
 
+    def set_wave_roles(self, roles: int = -1):
+        """mbik_plan_set_wave_roles: 1 one wave per segment role and a lane per skeleton
+        (64 skeletons per block, whole state in device memory), 0 off, -1 automatic."""
+        check(self._L.mbik_plan_set_wave_roles(self.h, int(roles)))
+
     def status(self) -> int:
         """mbik_plan_status: MBIK_STATUS_HELPER_TIMEOUT (1) when a completed helper-wave launch of
         this plan timed out in the two-wave handshake, else 0 (not cleared by reading)."""

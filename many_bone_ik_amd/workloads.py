@@ -209,7 +209,7 @@ def _realistic_rest(rng: SplitMix64, n: int, B: int, length: np.ndarray, q_rest:
     stream is untouched), for every bone b:
       offset direction: tilt ~ U[0, 110 deg] away from +Y, azimuth ~ U[0, 2pi)  (2 draws)
       roll about the bone's own +Y ~ U[-180, 180 deg)                            (1 draw)
-      uniform scale ~ U[0.6, 1.6], then per-axis factors ~ U[0.8, 1.25]          (4 draws)
+      uniform scale ~ U[0.8, 1.25], then per-axis factors ~ U[0.9, 1.1]          (4 draws)
     An imported humanoid's hips, clavicles and fingers sit off +Y, so
     update_default_bone_direction_transform (ik_bone_3d.cpp:57-93) takes the general arc
     branch; the rolls and non-uniform scales reach get_rotation_quaternion's

@@ -1,5 +1,6 @@
-"""Time mbik_solve under explicit layouts: args cfg:n:lanes:spw:interval[:placement:staging:waves] (0 = auto;
-placement / staging / waves default to the plan's own)."""
+"""Time mbik_solve under explicit layouts: args cfg:n:lanes:spw:interval[:placement:staging:waves[:roles]]
+(0 = auto; placement / staging / waves / wave roles default to the plan's own).  Every layout's
+output is compared bitwise with the first layout's of the same (cfg, n): `same` in the line."""
 import sys, json
 import torch
 sys.path.insert(0, '.')
@@ -8,6 +9,7 @@ from many_bone_ik_amd.solver import Plan
 
 dev = torch.device('cuda', 0)
 cache = {}
+first_out = {}
 for arg in sys.argv[1:]:
     f = [int(x) for x in arg.split(':')]
     cfg, n, lanes, spw, interval = f[:5]
@@ -23,6 +25,8 @@ for arg in sys.argv[1:]:
         p.set_heading_staging(f[6])
     if len(f) > 7:
         p.set_waves_per_simd(f[7])
+    if len(f) > 8:
+        p.set_wave_roles(f[8])
     pi = torch.from_numpy(wl.pose).to(dev); tg = torch.from_numpy(wl.targets).to(dev); po = torch.empty_like(pi)
     st = torch.cuda.current_stream(dev).cuda_stream
     p.solve(pi.data_ptr(), tg.data_ptr(), po.data_ptr(), 0, n, st); torch.cuda.synchronize()
@@ -34,6 +38,9 @@ for arg in sys.argv[1:]:
     e1.record(); torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / reps
     inf = p.info()
+    out = po.cpu()
+    same = bool(torch.equal(out.view(torch.int32), first_out.setdefault((cfg, n), out).view(torch.int32)))
     print(json.dumps(dict(arg=arg, lanes=inf['lanes_per_skeleton'], spw=inf['skeletons_per_block'],
-                          lds=inf['lds_bytes_per_block'], ms=round(ms, 3), mskel_s=round(n / ms / 1e3, 3))), flush=True)
+                          roles=inf.get('wave_roles', 0), wps=inf['waves_per_simd'], pl=inf['state_placement'],
+                          lds=inf['lds_bytes_per_block'], ms=round(ms, 3), mskel_s=round(n / ms / 1e3, 3), same=same)), flush=True)
     p.close()
