@@ -379,6 +379,27 @@ int32_t mbik_describe_topology(const mbik_skeleton_desc *desc, const mbik_config
  * exactly one of them is NaN.  Both must be 0 (gd_math.h: gd_sqrt). */
 int32_t mbik_selftest_math(int32_t device, uint64_t out[2]);
 
+/* Device known-answer tests (ABI 8): the solve kernel's own device functions on the inputs of
+ * the reference's unit tests (tests/test_qcp.h:40-113, tests/test_ik_kusudama_3d.h:38-156,
+ * tests/test_ik_node_3d.h:39-106), so the HIP code itself -- not only the CPU oracle -- is
+ * checked against their expectations.
+ * mbik_selftest_qcp: QCP::weighted_superpose + get_translation (qcp.cpp:220-248, 135-137) of n
+ *   pairs (moved, target: [n][3]; weights [n]), with eigenvector precision `precision` (the solve
+ *   uses 1e-6, ik_bone_segment_3d.h:85), through the primitives of the solve's one-lane heading
+ *   branch: out[0..3] the rotation (x, y, z, w), out[4..6] the translation; out[7..13] the same
+ *   from the select-form normalizations of the one-wave builds.
+ * mbik_selftest_point_in_limits: IKKusudama3D::get_local_point_in_limits (ik_kusudama_3d.cpp:
+ *   273-332) through the solve's own local_point_in_limits on the plan's setup tables (constraint
+ *   slot `slot`, i.e. the slot-th constraint on a bone of the IK bone list, of skeleton
+ *   `skeleton`): out[0..2] / in_bounds[0] the plain form, out[3..5] / in_bounds[1] the select form.
+ * mbik_selftest_xform: Transform3D as the IKNode3D tree uses it (ik_node_3d.cpp:56-113), 12 floats
+ *   (basis rows, origin): op 0 out = a * b, op 1 out = a.affine_inverse() (b unused). */
+int32_t mbik_selftest_qcp(int32_t n, const float *moved, const float *target, const double *weights, int32_t translate,
+		double precision, int32_t device, float out[14]);
+int32_t mbik_selftest_point_in_limits(const mbik_plan *plan, int32_t slot, int32_t skeleton, const float point[3], float out[6],
+		double in_bounds[2]);
+int32_t mbik_selftest_xform(int32_t op, const float a[12], const float b[12], int32_t device, float out[12]);
+
 /* Device self-test of the kernel's float quotients (gd_math.h: an fp64 reciprocal with a
  * residual correction, or one rounding for power-of-two numerators) against IEEE division:
  * out[c] = mismatching results of class c below (two NaNs compare equal), out[8 + 2c] and

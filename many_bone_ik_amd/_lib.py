@@ -33,7 +33,7 @@ EXPORTED_SYMBOLS = (
     "mbik_plan_status", "mbik_plan_debug_helper",
     "mbik_solve", "mbik_solve_checked", "mbik_solve_host", "mbik_segment_solve", "mbik_plan_segment_table", "mbik_describe_topology",
     "mbik_group_create", "mbik_group_solve", "mbik_group_destroy", "mbik_capture_targets", "mbik_selftest_math",
-    "mbik_selftest_libm", "mbik_selftest_div", "mbik_selftest_topology", "mbik_plan_create_device", "mbik_last_error",
+    "mbik_selftest_libm", "mbik_selftest_div", "mbik_selftest_qcp", "mbik_selftest_point_in_limits", "mbik_selftest_xform", "mbik_selftest_topology", "mbik_plan_create_device", "mbik_last_error",
 )
 
 
@@ -164,6 +164,14 @@ def load():
     L.mbik_plan_create_device.restype = C.c_int32
     L.mbik_selftest_div.argtypes = [C.c_int32, C.c_uint64, C.POINTER(C.c_uint64)]
     L.mbik_selftest_div.restype = C.c_int32
+    if hasattr(L, "mbik_selftest_qcp"):  # (ABI 8; absent from older A/B builds)
+        fp = C.POINTER(C.c_float)
+        L.mbik_selftest_qcp.argtypes = [C.c_int32, fp, fp, C.POINTER(C.c_double), C.c_int32, C.c_double, C.c_int32, fp]
+        L.mbik_selftest_qcp.restype = C.c_int32
+        L.mbik_selftest_point_in_limits.argtypes = [vp, C.c_int32, C.c_int32, fp, fp, C.POINTER(C.c_double)]
+        L.mbik_selftest_point_in_limits.restype = C.c_int32
+        L.mbik_selftest_xform.argtypes = [C.c_int32, fp, fp, C.c_int32, fp]
+        L.mbik_selftest_xform.restype = C.c_int32
     L.mbik_selftest_libm.argtypes = [C.c_int32, C.c_uint64, C.c_uint64, vp, vp, C.POINTER(C.c_uint64), vp]
     L.mbik_selftest_libm.restype = C.c_int32
     L.mbik_solve_host.argtypes = [vp, C.c_int32, C.c_int32, vp, vp, vp]

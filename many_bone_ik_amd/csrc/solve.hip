@@ -425,7 +425,9 @@ __device__ __forceinline__ B3 slerp_weight0(const B3 &from_b, const SlerpTo &tt,
 struct QSums {
 	double xx, xy, xz, yx, yy, yz, zx, zy, zz, ss1, ss2;
 };
-__device__ __forceinline__ Q qcp_adjugate(const QSums &S) {
+// evec_prec: QCP's eigenvector precision (the solver's 1e-6, ik_bone_segment_3d.h:85; the
+// reference's unit tests pass their own, mbik_selftest_qcp).
+__device__ __forceinline__ Q qcp_adjugate(const QSums &S, double evec_prec = 1E-6) {
 	double E0 = (S.ss1 + S.ss2) * 0.5;
 	double xz_plus_zx = S.xz + S.zx, yz_plus_zy = S.yz + S.zy, xy_plus_yx = S.xy + S.yx;
 	double yz_minus_zy = S.yz - S.zy, xz_minus_zx = S.xz - S.zx, xy_minus_yx = S.xy - S.yx;
@@ -449,7 +451,7 @@ __device__ __forceinline__ Q qcp_adjugate(const QSums &S) {
 	double qy = a21 * a3244_4234 - a22 * a3144_4134 + a24 * a3142_4132;
 	double qz = -a21 * a3243_4233 + a22 * a3143_4133 - a23 * a3142_4132;
 	double qsqr = qw * qw + qx * qx + qy * qy + qz * qz;
-	if (qsqr < 1E-6) return qid();
+	if (qsqr < evec_prec) return qid();
 	qx *= -1;
 	qy *= -1;
 	qz *= -1;
@@ -1096,7 +1098,9 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, int xs
 		V3 mvd = H.hm[0], tgt = H.ht[0];
 		if (translate) {
 			double w = H.w[0];
-			V3 mc = H.hm[0] * (float)w, tc = H.ht[0] * (float)w;
+			// move_to_weighted_center (qcp.cpp:139-160) accumulates from zero: 0 + p*w (a -0
+			// component comes out +0)
+			V3 mc = v3(0, 0, 0) + H.hm[0] * (float)w, tc = v3(0, 0, 0) + H.ht[0] * (float)w;
 			if (w > 0) {
 				mc = divs(mc, (float)w);
 				tc = divs(tc, (float)w);
@@ -3897,6 +3901,76 @@ int32_t mbik_plan_debug_helper(mbik_plan *p, int32_t drop_record, int32_t timeou
 
 } // extern "C"
 namespace {
+// ---- Device known-answer tests: the solve kernel's own device functions on the reference's
+// unit-test inputs (tests/golden/reference_kats.json: tests/test_qcp.h, test_ik_kusudama_3d.h,
+// test_ik_node_3d.h), so the HIP code -- not only the oracle -- is pinned to the reference. ----
+// QCP::weighted_superpose + get_translation (qcp.cpp:220-248, 135-137) with the primitives and the
+// order of bone_step's one-lane branch: the centroids accumulated from zero in float with a
+// double weight sum and divided through divs, the fp64 inner-product sums of qcp_accumulate in
+// heading order, then qcp_single (one pair) or qcp_adjugate.  out: quaternion (x, y, z, w) and
+// translation, for the plain (SEL false) and the select-form (SEL true) normalizations.
+template <bool SEL>
+__device__ void kat_qcp(const float *mv, const float *tg, const double *w, int n, int translate, double prec, float *out) {
+	auto M = [&](int i) { return v3(mv[3 * i], mv[3 * i + 1], mv[3 * i + 2]); };
+	auto T = [&](int i) { return v3(tg[3 * i], tg[3 * i + 1], tg[3 * i + 2]); };
+	V3 mc = v3(0, 0, 0), tc = v3(0, 0, 0);
+	if (translate) {
+		double wsum = 0;
+		for (int i = 0; i < n; i++) {
+			mc = mc + M(i) * (float)w[i];
+			tc = tc + T(i) * (float)w[i];
+			wsum += w[i];
+		}
+		if (wsum > 0) {
+			mc = divs(mc, (float)wsum);
+			tc = divs(tc, (float)wsum);
+		}
+	}
+	const V3 nmc = mc * -1.0f, ntc = tc * -1.0f;
+	QSums S = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+	for (int i = 0; i < n; i++) {
+		const V3 c1 = translate ? T(i) + ntc : T(i), c2 = translate ? M(i) + nmc : M(i);
+		qcp_accumulate(S, c1 * (float)w[i], c1, c2, w[i]);
+	}
+	Q q;
+	if (n == 1) q = qcp_single<SEL>(translate ? M(0) + nmc : M(0), translate ? T(0) + ntc : T(0));
+	else q = qcp_adjugate(S, prec);
+	const V3 tr = tc - mc;
+	out[0] = q.x; out[1] = q.y; out[2] = q.z; out[3] = q.w;
+	out[4] = tr.x; out[5] = tr.y; out[6] = tr.z;
+}
+__global__ __launch_bounds__(64) void mbik_kat_qcp_kernel(const float *mv, const float *tg, const double *w, int n, int translate,
+		double prec, float *out) {
+	if (threadIdx.x == 0) kat_qcp<false>(mv, tg, w, n, translate, prec, out);
+	if (threadIdx.x == 1) kat_qcp<true>(mv, tg, w, n, translate, prec, out + 7);
+}
+// IKKusudama3D::get_local_point_in_limits (ik_kusudama_3d.cpp:273-332) through the solve's own
+// local_point_in_limits on a plan's setup tables (constraint slot `slot` of skeleton s), both
+// normalization forms.  out: point (3) + in_bounds (as float) per form.
+__global__ __launch_bounds__(64) void mbik_kat_limits_kernel(DevPlan t, int slot, int s, float px, float py, float pz, float *out,
+		double *ib) {
+	double in_bounds = 1.0;
+	V3 r;
+	if (threadIdx.x == 0) r = local_point_in_limits<kTab64, false>(t, slot, (size_t)s, v3(px, py, pz), in_bounds);
+	else if (threadIdx.x == 1) r = local_point_in_limits<kTab64, true>(t, slot, (size_t)s, v3(px, py, pz), in_bounds);
+	else return;
+	out[3 * threadIdx.x] = r.x;
+	out[3 * threadIdx.x + 1] = r.y;
+	out[3 * threadIdx.x + 2] = r.z;
+	ib[threadIdx.x] = in_bounds;
+}
+// Transform3D ops of the IKNode3D tree (ik_node_3d.cpp:56-113): op 0 a * b, op 1 a.affine_inverse().
+__global__ __launch_bounds__(64) void mbik_kat_xform_kernel(int op, const float *a, const float *b, float *out) {
+	if (threadIdx.x != 0) return;
+	auto X = [](const float *v) { return X3{bset(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], v[8]), v3(v[9], v[10], v[11])}; };
+	const X3 r = op == 0 ? X(a) * X(b) : affine_inverse(X(a));
+	const float v[12] = {r.b.r[0].x, r.b.r[0].y, r.b.r[0].z, r.b.r[1].x, r.b.r[1].y, r.b.r[1].z,
+			r.b.r[2].x, r.b.r[2].y, r.b.r[2].z, r.o.x, r.o.y, r.o.z};
+	for (int i = 0; i < 12; i++) out[i] = v[i];
+}
+} // namespace
+
+namespace {
 __global__ void mbik_selftest_math_kernel(unsigned long long *out) {
 	const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
 	unsigned long long bad = 0, nan_bad = 0;
@@ -4070,6 +4144,79 @@ int32_t mbik_selftest_math(int32_t device, uint64_t out[2]) {
 	out[0] = h[0];
 	out[1] = h[1];
 	return rc;
+}
+
+// A device buffer of n bytes holding the host data (or zeroed): the KAT entry points' staging.
+namespace {
+struct DevBuf {
+	void *p = nullptr;
+	~DevBuf() {
+		if (p) (void)hipFree(p);
+	}
+	int put(const void *h, size_t n) {
+		if (hipMalloc(&p, std::max<size_t>(n, 8)) != hipSuccess) return fail(MBIK_ENOMEM, "hipMalloc");
+		if (h ? hipMemcpy(p, h, n, hipMemcpyHostToDevice) != hipSuccess : hipMemset(p, 0, std::max<size_t>(n, 8)) != hipSuccess)
+			return fail(MBIK_EHIP, "hipMemcpy");
+		return MBIK_OK;
+	}
+};
+int kat_device(int32_t device) {
+	int ndev = 0;
+	if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(MBIK_ENODEV, "no HIP device");
+	if (device < 0 || device >= ndev) return fail(MBIK_EINVAL, "device out of range");
+	return MBIK_OK;
+}
+int kat_finish(void *dst, const DevBuf &b, size_t n) {
+	if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) return fail(MBIK_EHIP, "KAT kernel");
+	if (hipMemcpy(dst, b.p, n, hipMemcpyDeviceToHost) != hipSuccess) return fail(MBIK_EHIP, "hipMemcpy");
+	return MBIK_OK;
+}
+} // namespace
+
+int32_t mbik_selftest_qcp(int32_t n, const float *moved, const float *target, const double *weights, int32_t translate,
+		double precision, int32_t device, float out[14]) {
+	if (n < 1 || !moved || !target || !weights || !out) return fail(MBIK_EINVAL, "n >= 1 and non-null buffers");
+	if (int rc = kat_device(device)) return rc;
+	DeviceGuard guard(device);
+	DevBuf m, t, w, o;
+	int rc = m.put(moved, 12 * (size_t)n);
+	if (!rc) rc = t.put(target, 12 * (size_t)n);
+	if (!rc) rc = w.put(weights, 8 * (size_t)n);
+	if (!rc) rc = o.put(nullptr, 14 * sizeof(float));
+	if (rc) return rc;
+	hipLaunchKernelGGL(mbik_kat_qcp_kernel, dim3(1), dim3(64), 0, 0, (const float *)m.p, (const float *)t.p, (const double *)w.p, n,
+			translate, precision, (float *)o.p);
+	return kat_finish(out, o, 14 * sizeof(float));
+}
+
+int32_t mbik_selftest_point_in_limits(const mbik_plan *p, int32_t slot, int32_t skeleton, const float point[3], float out[6],
+		double in_bounds[2]) {
+	if (!p || !point || !out || !in_bounds) return fail(MBIK_EINVAL, "null argument");
+	if (slot < 0 || slot >= p->host.NC || skeleton < 0 || skeleton >= p->host.N) return fail(MBIK_EINVAL, "slot or skeleton out of range");
+	DeviceGuard guard(p->device);
+	DevBuf o, ib;
+	int rc = o.put(nullptr, 6 * sizeof(float));
+	if (!rc) rc = ib.put(nullptr, 2 * sizeof(double));
+	if (rc) return rc;
+	DevPlan d = p->dev; // the plain [item][field][N] tables (kTab64)
+	hipLaunchKernelGGL(mbik_kat_limits_kernel, dim3(1), dim3(64), 0, 0, d, slot, skeleton, point[0], point[1], point[2], (float *)o.p,
+			(double *)ib.p);
+	if ((rc = kat_finish(out, o, 6 * sizeof(float))) != MBIK_OK) return rc;
+	if (hipMemcpy(in_bounds, ib.p, 2 * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) return fail(MBIK_EHIP, "hipMemcpy");
+	return MBIK_OK;
+}
+
+int32_t mbik_selftest_xform(int32_t op, const float a[12], const float b[12], int32_t device, float out[12]) {
+	if ((op != 0 && op != 1) || !a || (op == 0 && !b) || !out) return fail(MBIK_EINVAL, "op 0 (a * b) or 1 (affine_inverse(a)), non-null buffers");
+	if (int rc = kat_device(device)) return rc;
+	DeviceGuard guard(device);
+	DevBuf da, db, o;
+	int rc = da.put(a, 12 * sizeof(float));
+	if (!rc) rc = db.put(op == 0 ? b : a, 12 * sizeof(float));
+	if (!rc) rc = o.put(nullptr, 12 * sizeof(float));
+	if (rc) return rc;
+	hipLaunchKernelGGL(mbik_kat_xform_kernel, dim3(1), dim3(64), 0, 0, op, (const float *)da.p, (const float *)db.p, (float *)o.p);
+	return kat_finish(out, o, 12 * sizeof(float));
 }
 
 int32_t mbik_selftest_div(int32_t device, uint64_t random_iterations, uint64_t out[20]) {
