@@ -37,3 +37,15 @@ def test_oracle_reproduces_fixture(oracle, path):
     assert np.array_equal(r, f["seg_root"]) and np.array_equal(t, f["seg_tip"]) and np.array_equal(nh, f["seg_nh"])
     seg0 = o.segment_solve(0, wl.pose, wl.targets)
     assert np.array_equal(seg0.view(np.uint32), f["segment0_pose"].view(np.uint32))
+
+
+@pytest.mark.parametrize("path", FIX, ids=os.path.basename)
+def test_fixture_records_godot_version_and_oracle(path):
+    """SURVEY §7 hard part 1 / §8(c): every fixture names the Godot-core version its arithmetic
+    assumes and the oracle that produced it; the hash must be the current oracle's (an edited
+    oracle means: rerun tests/golden/make_golden.py)."""
+    from tests.golden.make_golden import GODOT_VERSION, oracle_source_hash
+    f = load(path)
+    assert str(f["godot_version"]) == GODOT_VERSION and str(f["godot_version"]).startswith("4.3")
+    assert str(f["oracle_sha256"]) == oracle_source_hash(), "oracle sources changed since the fixture was made"
+    assert "glibc 2.35" in str(f["libm"])
