@@ -54,6 +54,7 @@ extern "C" {
 
 typedef struct mbik_plan mbik_plan;
 typedef struct mbik_group mbik_group;
+typedef struct mbik_multi mbik_multi;
 
 /* == IKEffectorTemplate3D (src/ik_effector_template_3d.h:40-47). */
 typedef struct mbik_pin {
@@ -354,6 +355,34 @@ int32_t mbik_group_create(mbik_plan *const *plans, int32_t n_plans, mbik_group *
 int32_t mbik_group_solve(mbik_group *group, const int32_t *first, const int32_t *count, const float *const *pose_in,
 		const float *const *targets, float *const *pose_out, void *hip_stream);
 void mbik_group_destroy(mbik_group *group);
+
+/* Multi-GPU in one process (ABI 8): one batch of skeletons sharded over several
+ * plans, typically one per GPU, for an engine that is a single process (Godot is): contiguous
+ * shards in plan order -- plan i owns skeletons [off_i, off_i + N_i) of the batch, off_i the sum
+ * of the earlier plans' skeleton counts -- solved concurrently, each on its plan's device, with
+ * the poses gathered to the root device by peer copies over xGMI (no collective library: the
+ * solve has no exchange step).  The plans must agree on bone and pin counts (any topology,
+ * layout or setup data otherwise) and stay owned by the caller; they must outlive the handle and
+ * must not be solved elsewhere while a mbik_multi_solve on them is in flight.
+ *   flags MBIK_MULTI_STAGE_ALL: stage every shard through the handle's own device buffers, even a
+ *   shard whose plan lives on the root device (the copy path a one-GPU machine can test). */
+#define MBIK_MULTI_STAGE_ALL 1u
+int32_t mbik_multi_create(mbik_plan *const *plans, int32_t n_plans, int32_t root_device, uint32_t flags, mbik_multi **out);
+/* One frame of the whole batch.  pose_in / targets / pose_out are device buffers on the root
+ * device holding every skeleton ([total][bones][10], [total][pins][12]; pose_out may equal
+ * pose_in).  Asynchronous on root_stream (a stream of the root device, NULL = its default
+ * stream): each plan's work -- the copy of its shard to its device, its mbik_solve, the copy of
+ * its poses back into pose_out -- runs on a stream the handle owns on the plan's device, after
+ * everything already queued on root_stream, and root_stream waits for all of them, so work
+ * queued after the call sees the gathered poses.  Shards whose plan lives on the root device
+ * solve in place in the caller's buffers (unless MBIK_MULTI_STAGE_ALL).  Calls on one handle are
+ * ordered by root_stream; use one root stream per handle.  Returns the first error; a helper-wave
+ * timeout of any plan is reported as by mbik_solve. */
+int32_t mbik_multi_solve(mbik_multi *multi, const float *pose_in, const float *targets, float *pose_out, void *root_stream);
+/* The batch size (the plans' skeleton counts summed) and shard offsets (off[n_plans + 1],
+ * may be NULL). */
+int64_t mbik_multi_skeletons(const mbik_multi *multi, int64_t *off);
+void mbik_multi_destroy(mbik_multi *multi);
 
 /* Runs IKBoneSegment3D::segment_solver() once on `segment` (index in post-order segment
  * numbering of mbik_plan_segment_table) for every skeleton in [first, first+count), updating

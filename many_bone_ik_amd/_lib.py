@@ -17,6 +17,7 @@ MBIK_ENOMEM = -2
 MBIK_EHIP = -3
 MBIK_EUNSUPPORTED = -4
 MBIK_ENODEV = -5
+MBIK_MULTI_STAGE_ALL = 1
 
 # mbik_selftest_libm function codes (include/mbik.h)
 LIBM_SINF, LIBM_COSF, LIBM_ACOSF, LIBM_SLERP_SCALE0, LIBM_COS_F64_OF_F32, LIBM_COS_F64, LIBM_SINF_SSE2, LIBM_COSF_SSE2, \
@@ -32,7 +33,8 @@ EXPORTED_SYMBOLS = (
     "mbik_plan_set_locals_placement", "mbik_plan_set_waves_per_simd", "mbik_plan_set_helper_wave", "mbik_plan_set_wave_roles", "mbik_plan_set_table_addressing", "mbik_plan_rebuild_setup", "mbik_plan_setup_tables",
     "mbik_plan_status", "mbik_plan_debug_helper",
     "mbik_solve", "mbik_solve_checked", "mbik_solve_host", "mbik_segment_solve", "mbik_plan_segment_table", "mbik_describe_topology",
-    "mbik_group_create", "mbik_group_solve", "mbik_group_destroy", "mbik_capture_targets", "mbik_selftest_math",
+    "mbik_group_create", "mbik_group_solve", "mbik_group_destroy", "mbik_multi_create", "mbik_multi_solve",
+    "mbik_multi_skeletons", "mbik_multi_destroy", "mbik_capture_targets", "mbik_selftest_math",
     "mbik_selftest_libm", "mbik_selftest_div", "mbik_selftest_qcp", "mbik_selftest_point_in_limits", "mbik_selftest_xform", "mbik_selftest_topology", "mbik_plan_create_device", "mbik_last_error",
 )
 
@@ -188,6 +190,15 @@ def load():
     L.mbik_group_solve.restype = C.c_int32
     L.mbik_group_destroy.argtypes = [vp]
     L.mbik_group_destroy.restype = None
+    if hasattr(L, "mbik_multi_create"):  # (ABI 8; absent from older A/B builds)
+        L.mbik_multi_create.argtypes = [C.POINTER(vp), C.c_int32, C.c_int32, C.c_uint32, C.POINTER(vp)]
+        L.mbik_multi_create.restype = C.c_int32
+        L.mbik_multi_solve.argtypes = [vp, vp, vp, vp, vp]
+        L.mbik_multi_solve.restype = C.c_int32
+        L.mbik_multi_skeletons.argtypes = [vp, C.POINTER(C.c_int64)]
+        L.mbik_multi_skeletons.restype = C.c_int64
+        L.mbik_multi_destroy.argtypes = [vp]
+        L.mbik_multi_destroy.restype = None
     L.mbik_capture_targets.argtypes = [vp, C.c_int32, C.c_int32, vp, vp, vp, vp, vp]
     L.mbik_capture_targets.restype = C.c_int32
     L.mbik_last_error.argtypes = []

@@ -369,6 +369,41 @@ class Group:
             pass
 
 
+class Multi:
+    """mbik_multi_*: one batch sharded over several plans (one per GPU) in one process;
+    contiguous shards in plan order, poses gathered to the root device (peer copies)."""
+
+    def __init__(self, plans, root_device: int = 0, stage_all: bool = False):
+        self._L = _lib.load()
+        self.plans = list(plans)            # keeps the plans alive while the handle exists
+        arr = (C.c_void_p * len(self.plans))(*[p.h for p in self.plans])
+        h = C.c_void_p()
+        check(self._L.mbik_multi_create(arr, len(self.plans), int(root_device),
+                                        _lib.MBIK_MULTI_STAGE_ALL if stage_all else 0, C.byref(h)))
+        self.h = h
+
+    def skeletons(self):
+        """(total skeletons, shard offsets)."""
+        off = (C.c_int64 * (len(self.plans) + 1))()
+        n = self._L.mbik_multi_skeletons(self.h, off)
+        return int(n), [int(x) for x in off]
+
+    def solve(self, pose_in_ptr: int, targets_ptr: int, pose_out_ptr: int, root_stream: int = 0):
+        check(self._L.mbik_multi_solve(self.h, C.c_void_p(pose_in_ptr), C.c_void_p(targets_ptr),
+                                       C.c_void_p(pose_out_ptr), C.c_void_p(root_stream or None)))
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._L.mbik_multi_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def quat_error(a: np.ndarray, b: np.ndarray) -> np.ndarray:
     """Per-bone sign-invariant quaternion error min(|q-r|_inf, |q+r|_inf)."""
     qa = a[..., 0:4].astype(np.float64)

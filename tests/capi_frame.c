@@ -11,6 +11,10 @@
  *     read back                         <- _update_skeleton_bones_transform (:104-116)
  *   the frame's output pose is the next frame's input (the Skeleton3D pose the reference
  *   captures again, the warm start)
+ * and, when header[7] = S > 0, frame 0 once more through the single-process multi-GPU entry
+ * points: the batch split into S plans (contiguous shards), mbik_multi_create (root device 0,
+ * MBIK_MULTI_STAGE_ALL so the scatter / gather copies run even with one GPU) and
+ * mbik_multi_solve on the whole batch.
  *
  * Built by __graft_entry__.build() (many_bone_ik_amd/build.py: build_capi_frame) with gcc -std=c99
  * -Wall -Wextra -Werror; run by tests/test_capi_frame.py, which compares every frame bitwise
@@ -19,12 +23,12 @@
  *   capi_frame <input.bin> <output.bin>
  *
  * input.bin (little-endian): int32 header[8] = {bones B, pins P, constraints C, max_cones MC,
- * iterations, skeletons n, frames F, 0}; int32 parents[B]; int32 pin_bone[P]; float
+ * iterations, skeletons n, frames F, multi shards S}; int32 parents[B]; int32 pin_bone[P]; float
  * pin_weight[P]; float pin_priority[P][3]; float pin_propagation[P]; int32 cons_bone[C]; int32
  * cons_cones[C]; float default_damp; float setup_pose[n][B][10]; float cones[n][C][MC][4];
  * float twist[n][C][2]; float skeleton_global[n][12]; float target_global[F][n][P][12].
  * output.bin: per frame: float targets[n][P][12] (captured), float pose[n][B][10], uint8
- * nonfinite[n].
+ * nonfinite[n]; then, when S > 0, float pose[n][B][10] (frame 0 through mbik_multi_solve).
  */
 #include <hip/hip_runtime_api.h>
 #include <stdio.h>
@@ -88,7 +92,7 @@ int main(int argc, char **argv) {
 	fclose(f);
 
 	const int32_t *hdr = take(8 * sizeof(int32_t));
-	const int32_t B = hdr[0], P = hdr[1], C = hdr[2], MC = hdr[3], iterations = hdr[4], n = hdr[5], F = hdr[6];
+	const int32_t B = hdr[0], P = hdr[1], C = hdr[2], MC = hdr[3], iterations = hdr[4], n = hdr[5], F = hdr[6], S = hdr[7];
 	const int32_t *parents = take((size_t)B * 4);
 	const int32_t *pin_bone = take((size_t)P * 4);
 	const float *pin_weight = take((size_t)P * 4);
@@ -186,6 +190,35 @@ int main(int argc, char **argv) {
 			fprintf(stderr, "capi_frame: short write\n");
 			return 1;
 		}
+	}
+	if (S > 0) {
+		/* frame 0 again, sharded: S plans over contiguous skeleton ranges, one mbik_multi */
+		mbik_plan **shard = calloc((size_t)S, sizeof(mbik_plan *));
+		for (int k = 0; k < S; k++) {
+			const int32_t lo = (int32_t)((int64_t)n * k / S), hi = (int32_t)((int64_t)n * (k + 1) / S);
+			check_mbik(mbik_plan_create(&desc, &cfg, hi - lo, setup_pose + (size_t)lo * B * 10, C ? cones + (size_t)lo * C * MC * 4 : NULL,
+							   C ? twist + (size_t)lo * C * 2 : NULL, 0, &shard[k]),
+					"mbik_plan_create (shard)");
+		}
+		mbik_multi *multi = NULL;
+		check_mbik(mbik_multi_create(shard, S, 0, MBIK_MULTI_STAGE_ALL, &multi), "mbik_multi_create");
+		if (mbik_multi_skeletons(multi, NULL) != n) {
+			fprintf(stderr, "capi_frame: mbik_multi_skeletons != n\n");
+			return 7;
+		}
+		check_hip(hipMemcpyAsync(d_pose[0], setup_pose, pose_bytes, hipMemcpyHostToDevice, stream), "hipMemcpyAsync pose");
+		check_hip(hipMemcpyAsync(d_target_global, target_global, tg_bytes, hipMemcpyHostToDevice, stream), "hipMemcpyAsync targets");
+		check_mbik(mbik_capture_targets(plan, 0, n, d_skeleton_global, d_target_global, NULL, d_targets, stream), "mbik_capture_targets");
+		check_mbik(mbik_multi_solve(multi, d_pose[0], d_targets, d_pose[1], stream), "mbik_multi_solve");
+		check_hip(hipMemcpyAsync(h_pose, d_pose[1], pose_bytes, hipMemcpyDeviceToHost, stream), "hipMemcpyAsync D2H");
+		check_hip(hipStreamSynchronize(stream), "hipStreamSynchronize");
+		if (fwrite(h_pose, 1, pose_bytes, out) != pose_bytes) {
+			fprintf(stderr, "capi_frame: short write\n");
+			return 1;
+		}
+		mbik_multi_destroy(multi);
+		for (int k = 0; k < S; k++) mbik_plan_destroy(shard[k]);
+		free(shard);
 	}
 	fclose(out);
 	check_hip(hipFree(d_pose[0]), "hipFree");

@@ -15,7 +15,7 @@ HEADER = os.path.join(os.path.dirname(os.path.dirname(__file__)), "include", "mb
 
 def header_functions():
     src = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int32_t|void|const char \*)\s*(mbik_\w+)\(", src, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int32_t|int64_t|void|const char \*)\s*(mbik_\w+)\(", src, re.M)))
 
 
 def test_header_declares_and_library_exports_every_symbol(mbik):

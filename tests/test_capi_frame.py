@@ -30,13 +30,13 @@ def test_capi_frame_compiles_as_c99(mbik):
         assert r.returncode == 1 and "usage" in r.stderr
 
 
-def write_input(path, wl, skel_global, target_global):
+def write_input(path, wl, skel_global, target_global, shards=0):
     t = wl.topo
     P, C = t.pins.shape[0], t.constrained.shape[0]
     MC = wl.cones.shape[2]
     frames = target_global.shape[0]
     with open(path, "wb") as f:
-        np.array([wl.bone_count, P, C, MC, t.iterations, wl.n, frames, 0], np.int32).tofile(f)
+        np.array([wl.bone_count, P, C, MC, t.iterations, wl.n, frames, shards], np.int32).tofile(f)
         t.parents.astype(np.int32).tofile(f)
         t.pins.astype(np.int32).tofile(f)
         wl.pin_weight.astype(np.float32).tofile(f)
@@ -49,11 +49,12 @@ def write_input(path, wl, skel_global, target_global):
             np.ascontiguousarray(a, np.float32).tofile(f)
 
 
-def read_output(path, wl, frames):
+def read_output(path, wl, frames, shards=0):
     n, Bn, P = wl.n, wl.bone_count, wl.topo.pins.shape[0]
     raw = np.fromfile(path, np.uint8)
     per = n * P * 12 * 4 + n * Bn * 10 * 4 + n
-    assert raw.size == frames * per, (raw.size, frames * per)
+    multi = n * Bn * 40 if shards else 0
+    assert raw.size == frames * per + multi, (raw.size, frames * per + multi)
     out = []
     for f in range(frames):
         r = raw[f * per:(f + 1) * per]
@@ -61,12 +62,16 @@ def read_output(path, wl, frames):
         pose = r[n * P * 48:n * P * 48 + n * Bn * 40].view(np.float32).reshape(n, Bn, 10)
         nf = r[n * P * 48 + n * Bn * 40:]
         out.append((tg, pose, nf))
+    if shards:
+        out.append(raw[frames * per:].view(np.float32).reshape(n, Bn, 10))
     return out
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg,n,rest", [(2, 256, "plus_y"), (2, 128, "realistic"), (4, 32, "realistic")])
-def test_c_frame_loop_bitwise_vs_oracle(oracle, mbik, cfg, n, rest):
+@pytest.mark.parametrize("cfg,n,rest,shards", [(2, 256, "plus_y", 3), (2, 128, "realistic", 2), (4, 32, "realistic", 0)])
+def test_c_frame_loop_bitwise_vs_oracle(oracle, mbik, cfg, n, rest, shards):
+    """shards > 0: frame 0 once more through mbik_multi_create / mbik_multi_solve over that many
+    plans (the single-process multi-GPU entry points), equal to frame 0."""
     exe = B.CAPI_FRAME
     assert os.path.exists(exe), "tests/capi_frame not built: __graft_entry__.build() builds it"
     wl = W.generate(cfg, n, first=5000, rest=rest)
@@ -84,10 +89,11 @@ def test_c_frame_loop_bitwise_vs_oracle(oracle, mbik, cfg, n, rest):
                 tgl[f, s, e] = oracle.xform_mul(skel[s], drift[s, e])
     with tempfile.TemporaryDirectory() as d:
         fin, fout = os.path.join(d, "in.bin"), os.path.join(d, "out.bin")
-        write_input(fin, wl, skel, tgl)
+        write_input(fin, wl, skel, tgl, shards)
         r = subprocess.run([exe, fin, fout], capture_output=True, text=True, timeout=300)
         assert r.returncode == 0, r.stderr + r.stdout
-        got = read_output(fout, wl, frames)
+        got = read_output(fout, wl, frames, shards)
+    multi = got.pop() if shards else None
     o = oracle.Oracle(wl)
     pose = wl.pose
     for f, (tg, out, nf) in enumerate(got):
@@ -97,4 +103,6 @@ def test_c_frame_loop_bitwise_vs_oracle(oracle, mbik, cfg, n, rest):
         ref = o.solve(pose, want_tg, threads=8)
         assert_parity(out, ref, f"C frame loop, {rest} C{cfg}, frame {f}")
         assert not nf.any()
+        if f == 0 and multi is not None:
+            assert_parity(multi, ref, f"C mbik_multi_solve over {shards} plans, {rest} C{cfg}")
         pose = ref

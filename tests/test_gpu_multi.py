@@ -1,0 +1,73 @@
+"""Multi-GPU in the library: mbik_multi_create / mbik_multi_solve shard one
+batch over several plans -- contiguous skeleton ranges, each plan on its own device and a stream
+the handle owns -- and gather the poses to the root device (the per-frame call is
+many_bone_ik_3d.cpp:645-694).  On the one-GPU box the plans share device 0: without staging the
+shards solve in place on concurrent streams, and MBIK_MULTI_STAGE_ALL runs the scatter / solve /
+gather copy path that separate devices use.  Bitwise against the oracle.  Needs an MI355X: -m gpu."""
+import numpy as np
+import pytest
+
+from many_bone_ik_amd import _lib
+from many_bone_ik_amd import workloads as W
+from many_bone_ik_amd.solver import Multi, Plan
+
+from .test_gpu_parity import assert_parity, torch_dev  # noqa: F401 (fixture)
+
+pytestmark = pytest.mark.gpu
+
+
+def shard_plans(wl, cuts, **kw):
+    """One plan per contiguous range [cuts[i], cuts[i+1]) of the workload's skeletons."""
+    return [Plan(wl.topo.parents, wl.pins(), wl.constraints(), wl.pose[lo:hi], wl.cones[lo:hi], wl.twist[lo:hi],
+                 iterations=wl.topo.iterations, default_damp=wl.default_damp, max_cones=wl.cones.shape[2], **kw)
+            for lo, hi in zip(cuts[:-1], cuts[1:])]
+
+
+@pytest.mark.parametrize("cfg,n,cuts", [(2, 300, [0, 100, 300]), (4, 130, [0, 64, 65, 130]), (5, 40, [0, 13, 26, 40])])
+@pytest.mark.parametrize("stage_all", [False, True])
+def test_multi_solve_bitwise_vs_oracle(oracle, mbik, torch_dev, cfg, n, cuts, stage_all):
+    torch, dev = torch_dev
+    wl = W.generate(cfg, n, first=61000 + cfg)
+    ref = oracle.Oracle(wl).solve(wl.pose, wl.targets, threads=8)
+    plans = shard_plans(wl, cuts)
+    m = Multi(plans, root_device=0, stage_all=stage_all)
+    assert m.skeletons() == (n, cuts)
+    pi = torch.from_numpy(wl.pose).to(dev)
+    tg = torch.from_numpy(wl.targets).to(dev)
+    po = torch.full_like(pi, float("nan"))
+    st = torch.cuda.Stream(dev)
+    for _ in range(2):                   # twice: the handle's streams and events are reused
+        m.solve(pi.data_ptr(), tg.data_ptr(), po.data_ptr(), st.cuda_stream)
+        st.synchronize()
+        assert_parity(po.cpu().numpy(), ref, f"C{cfg} multi over {len(plans)} plans stage_all={stage_all}")
+
+
+def test_multi_in_place_and_stream_order(oracle, mbik, torch_dev):
+    """pose_out == pose_in, with work queued on the root stream before and after the call."""
+    torch, dev = torch_dev
+    wl = W.generate(2, 200, first=62000)
+    ref = oracle.Oracle(wl).solve(wl.pose, wl.targets, threads=8)
+    m = Multi(shard_plans(wl, [0, 77, 200]), stage_all=True)
+    st = torch.cuda.Stream(dev)
+    with torch.cuda.stream(st):
+        pose = torch.zeros(wl.pose.shape, dtype=torch.float32, device=dev)
+        pose.copy_(torch.from_numpy(wl.pose).to(dev, non_blocking=True))       # queued before the solve
+        tg = torch.from_numpy(wl.targets).to(dev)
+        m.solve(pose.data_ptr(), tg.data_ptr(), pose.data_ptr(), st.cuda_stream)
+        after = pose.clone()                                                   # queued after it
+    st.synchronize()
+    assert_parity(after.cpu().numpy(), ref, "multi in place")
+
+
+def test_multi_argument_checks(mbik):
+    a = Plan.from_workload(W.generate(2, 8))
+    b = Plan.from_workload(W.generate(3, 8))
+    c = Plan.from_workload(W.generate(4, 8))              # 64 bones: not the same shape
+    for plans, root in ([a, a], 0), ([a, c], 0), ([a, b], 99):
+        with pytest.raises(_lib.MbikError) as e:
+            Multi(plans, root_device=root)
+        assert e.value.code == _lib.MBIK_EINVAL
+    m = Multi([a, b])
+    assert m.skeletons() == (16, [0, 8, 16])
+    with pytest.raises(_lib.MbikError):
+        m.solve(0, 0, 0)
