@@ -3949,6 +3949,11 @@ __global__ __launch_bounds__(64) void mbik_kat_qcp_kernel(const float *mv, const
 // normalization forms.  out: point (3) + in_bounds (as float) per form.
 __global__ __launch_bounds__(64) void mbik_kat_limits_kernel(DevPlan t, int slot, int s, float px, float py, float pz, float *out,
 		double *ib) {
+	// the topology tables straight from the plan's blob in device memory (the solve copies it to LDS)
+	const uint32_t *topo = reinterpret_cast<const uint32_t *>(t.topo_blob);
+#define MBIK_REPOINT(T, name) t.name = reinterpret_cast<const T *>(topo + t.o_##name);
+	MBIK_TOPO_TABLES(MBIK_REPOINT)
+#undef MBIK_REPOINT
 	double in_bounds = 1.0;
 	V3 r;
 	if (threadIdx.x == 0) r = local_point_in_limits<kTab64, false>(t, slot, (size_t)s, v3(px, py, pz), in_bounds);
@@ -4194,6 +4199,9 @@ int32_t mbik_selftest_point_in_limits(const mbik_plan *p, int32_t slot, int32_t 
 	if (!p || !point || !out || !in_bounds) return fail(MBIK_EINVAL, "null argument");
 	if (slot < 0 || slot >= p->host.NC || skeleton < 0 || skeleton >= p->host.N) return fail(MBIK_EINVAL, "slot or skeleton out of range");
 	DeviceGuard guard(p->device);
+	// the topology blob the kernel reads (uploaded with the launch schedule)
+	if (int rc = ensure_schedule(const_cast<mbik_plan *>(p), p->host.N)) return rc;
+	if (!p->dev.topo_blob) return fail(MBIK_EHIP, "plan has no topology blob");
 	DevBuf o, ib;
 	int rc = o.put(nullptr, 6 * sizeof(float));
 	if (!rc) rc = ib.put(nullptr, 2 * sizeof(double));

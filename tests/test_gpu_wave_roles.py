@@ -84,7 +84,7 @@ def test_wave_roles_fuzz_rigs(oracle, mbik):
     schedule's rows and packed levels over the waves, whatever their shape."""
     from .test_gpu_fuzz import random_case
     for seed in range(12):
-        wl = random_case(seed)
+        wl, _, _ = random_case(seed)          # (stabilization excluded: wave roles refuse it)
         ref = oracle.Oracle(wl).solve(wl.pose, wl.targets, threads=8)
         for k, wps in [(2, 1), (4, 2)]:
             plan = rw_plan(wl, k, wps)
@@ -149,7 +149,10 @@ def test_wave_roles_nonfinite_flags(oracle, mbik, torch_dev):
         torch.cuda.synchronize()
         outs.append(po.cpu().numpy())
         flags.append(f.cpu().numpy())
-    assert np.array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32))
+    # (NaN payloads may differ between builds; test_gpu_realistic compares NaN placement too)
+    nan0, nan1 = np.isnan(outs[0]), np.isnan(outs[1])
+    assert np.array_equal(nan0, nan1)
+    assert np.array_equal(outs[0][~nan0].view(np.uint32), outs[1][~nan1].view(np.uint32))
     assert np.array_equal(flags[0], flags[1]) and set(np.unique(flags[1])) <= {0, 1}
     assert flags[1].sum() > 0
 
