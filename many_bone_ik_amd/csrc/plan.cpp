@@ -669,10 +669,24 @@ void build_schedule(HostPlan &p, int32_t lanes, int64_t nlaunch, int32_t spw_ove
 			int cnt = (int)std::min<size_t>(K, l.size() - start);
 			int m = K >> ceil_log2(cnt);
 			if (p.wave_roles) {
-				// Wave roles: one wave per segment (no group of lanes repeating its work); the
-				// row's segments spread over the block's waves, the others wait at the row barrier.
+				// Wave roles: each segment of the row on a group of m waves.  A segment of two or
+				// more effectors is solved cooperatively (SCHED_XS): its waves split the effector path
+				// walks and its first wave runs the rest of each bone-step once; a single-effector
+				// segment runs on the group's first wave alone.  No wave repeats another's work.
 				std::vector<SchedTask> row(K, SchedTask{-1, 0, 1, 0});
-				for (int i = 0; i < cnt; i++) row[i * m] = SchedTask{l[start + i], 0, 1, 0};
+				bool coop = false;
+				for (int i = 0; i < cnt; i++) {
+					const int sg = l[start + i];
+					const bool multi = p.seg_eff_off[sg + 1] - p.seg_eff_off[sg] >= 2;
+					if (multi && m >= 2) {
+						for (int j = 0; j < m; j++) row[i * m + j] = SchedTask{sg, j, m, SCHED_XS};
+						coop = true;
+					} else {
+						row[i * m] = SchedTask{sg, 0, 1, 0};
+					}
+				}
+				if (coop)
+					for (auto &tk : row) tk.flags |= SCHED_COOP;
 				p.sched.insert(p.sched.end(), row.begin(), row.end());
 				p.nrows++;
 				continue;
@@ -706,7 +720,22 @@ void build_schedule(HostPlan &p, int32_t lanes, int64_t nlaunch, int32_t spw_ove
 	// offsets restart at every row.
 	p.seg_hbase.assign(p.NS, 0);
 	p.hs_floats = 0;
-	for (int r = 0; r < p.nrows; r++) {
+	p.rw_xslots = 0;
+	if (p.wave_roles) {
+		// wave roles: a cooperative segment's effector globals go through LDS, one slot per
+		// effector; the segments of a row run concurrently, so their slots are disjoint
+		for (int r = 0; r < p.nrows; r++) {
+			int used = 0;
+			for (int l = 0; l < K; l++) {
+				const SchedTask &tk = p.sched[(size_t)r * K + l];
+				if (tk.seg < 0 || tk.j != 0 || !(tk.flags & SCHED_XS)) continue;
+				p.seg_hbase[tk.seg] = used;
+				used += p.seg_eff_off[tk.seg + 1] - p.seg_eff_off[tk.seg];
+			}
+			p.rw_xslots = std::max(p.rw_xslots, used);
+		}
+	}
+	for (int r = 0; r < p.nrows && !p.wave_roles; r++) {
 		int used = 0;
 		for (int l = 0; l < K; l++) {
 			const SchedTask &tk = p.sched[(size_t)r * K + l];
@@ -813,7 +842,8 @@ void build_schedule(HostPlan &p, int32_t lanes, int64_t nlaunch, int32_t spw_ove
 		r[3] = c0 | ((c1 - c0) << 16);
 	}
 	p.spw = best;
-	p.lds_block_bytes = best * (int64_t)(((lds_floats_per_skeleton(p) + 3) & ~3) * 4) + topo + (p.wave_roles ? 64 * 4 : 0);
+	p.lds_block_bytes = best * (int64_t)(((lds_floats_per_skeleton(p) + 3) & ~3) * 4) + topo +
+			(p.wave_roles ? 64 * 4 + (int64_t)p.rw_xslots * 12 * 64 * 4 : 0);
 }
 
 } // namespace mbik

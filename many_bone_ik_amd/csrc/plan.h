@@ -62,7 +62,11 @@ struct SchedTask {
 	               // headings and share them through cross-lane reads; every lane sums them all in order (no
 	               // staging memory).  bit 1 (SCHED_CHAIN): this row continues the previous one's packed level
 };
-constexpr int32_t SCHED_XS = 1, SCHED_CHAIN = 2;
+// SCHED_COOP (wave roles only): every task of this row carries it when some segment of the row is
+// solved by a group of waves (SCHED_XS, m > 1): the group's waves walk alternate effectors' paths
+// and leave the effector globals in LDS, the group's first wave consumes them all in order and runs
+// the step's rotation chain; the whole block meets at two barriers per bone-step of the row.
+constexpr int32_t SCHED_XS = 1, SCHED_CHAIN = 2, SCHED_COOP = 4;
 
 struct HostPlan {
 	// ---- topology (shared by the batch) ----
@@ -128,6 +132,9 @@ struct HostPlan {
 	// segment runs on one wave with its topology wave-uniform and no lane of a skeleton repeats
 	// another's work.  Whole state in device memory (state_hbm 2).  0: roles are lanes of a wave.
 	int32_t wave_roles = 0;
+	// wave roles: effector-global exchange slots of the cooperative rows (SCHED_COOP), the most any
+	// row needs; a slot is 12 floats x 64 lanes of LDS.  seg_hbase[seg] is the segment's first slot.
+	int32_t rw_xslots = 0;
 	// Iteration-start globals kept in LDS only for checkpoint bones: every g_interval-th bone
 	// of a segment counted from its root (the root included) and every parent of a segment
 	// root; a bone-step rebuilds its parent's global from the nearest checkpoint above it.

@@ -80,6 +80,7 @@ struct DevPlan {
 	int stab;            // stabilization_passes (root segments only, SF_STAB)
 	int prio_mask = 0;   // kPrioDefault if every effector has that heading slot mask, else 0
 	int hs_floats;       // staged-heading LDS floats per skeleton
+	int rw_xslots = 0;   // wave roles: effector-global exchange slots (12 floats x 64 lanes of LDS each)
 	int n_gck;           // checkpoint globals per skeleton (HostPlan::bone_gslot)
 	int constraint_mode; // ManyBoneIK3D::constraint_mode
 	int libm;            // the reference host's glibc sinf/cosf build (gd::LIBM_FMA / LIBM_SSE2)
@@ -513,13 +514,14 @@ __device__ __forceinline__ bool prio_on(float pr, int a) {
 	if constexpr (PM != 0) return ((PM >> (1 + 2 * a)) & 1) != 0;
 	else return pr > 0.0f;
 }
-template <int TA, int PM = 0, class FP>
+// DB false: without the effector bone's bone-direction basis (only a path walk reads it).
+template <int TA, int PM = 0, bool DB = true, class FP>
 __device__ __forceinline__ void load_eff(const DevPlan &t, int e, const FP TG, size_t s, const double *hw, EffPre &p) {
 	p.e = e;
 	p.off = t.eff_path_off[e];
 	p.de = t.eff_path_off[e + 1] - p.off - 1;
 	p.T = ld_x(TG + 12 * e);
-	p.Db = ld_soa_basis<TA>(t, t.D, t.eff_bone[e], 9, 0, s);
+	if constexpr (DB) p.Db = ld_soa_basis<TA>(t, t.D, t.eff_bone[e], 9, 0, s);
 	p.hws[0] = hw[0];
 	int k = 1;
 #pragma unroll
@@ -1037,10 +1039,12 @@ __device__ __forceinline__ void qcp_accumulate(QSums &S, const V3 wc1, const V3 
 // stride 64), not from this wave.  XS: the build serves split-exchange tasks (xs, staging 4 /
 // 5): only the two-waves-per-SIMD build, so that the one-wave kernels keep their registers.
 // SEL: the orthonormalizations' zero-vector tests as selects (normalized_sel; the one-wave builds).
-template <bool STAB, bool PR, int TA, bool HELP, bool XS, int PM, bool SEL, class LV, class GV, class FP, class IP>
+// XW (wave roles): xs marks a cooperative segment whose effector globals the group's waves left in
+// the exchange area xw (coop_walk); this wave, the group's first, consumes them.
+template <bool STAB, bool PR, int TA, bool HELP, bool XS, int PM, bool SEL, bool XW, class LV, class GV, class FP, class IP>
 __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, int xs, size_t s, const LV &L, const GV &G, const FP TG,
 		const FP ST, const IP SF, const FP HS, const FP OE, const FP MS, double &prev_dev, const EffPre &pre, bool hoist,
-		const float4 *hrec, int *hfl, int hseq, bool *hstuck MBIK_PROF_PARAM) {
+		const float4 *hrec, int *hfl, int hseq, bool *hstuck, const float *xw MBIK_PROF_PARAM) {
 	MBIK_PROF_T(pt0);
 #ifdef MBIK_PROF
 	uint64_t pt1 = pt0, pt3 = pt0;
@@ -1110,6 +1114,52 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, int xs
 			translation = tc - mc;
 		}
 		qrot = qcp_single<SEL>(mvd, tgt);
+	} else if (XW && xs) {
+		// Wave roles, cooperative segment: every effector's bone-direction global E comes from the
+		// block's exchange area, where the group's waves left it after walking its path from this
+		// step's Gb (coop_walk, the same products as effector_headings).  The headings are built
+		// from E in the reference's effector order and summed as the one-lane branch below does,
+		// so every sum rounds the same; a translating segment builds them twice, as
+		// weighted_superpose does (qcp.cpp:220-248).
+		const float *xe = xw + (size_t)t.seg_hbase[seg] * (12 * 64) + __lane_id();
+		auto each = [&](auto &&use) __attribute__((always_inline)) {
+			for (int i = e0; i < e1; i++) {
+				EffPre p;
+				load_eff<TA, PM, false>(t, t.seg_effs[i], TG, s, hw + t.seg_eff_hoff[i], p);
+				const float *r = xe + (size_t)(i - e0) * (12 * 64);
+				X3 E;
+				E.b.r[0] = v3(r[0], r[64], r[128]);
+				E.b.r[1] = v3(r[192], r[256], r[320]);
+				E.b.r[2] = v3(r[384], r[448], r[512]);
+				E.o = v3(r[576], r[640], r[704]);
+				Headings Hm;
+				heading_terms<PM>(p, E, E.o, Gb.o, Hm);
+#pragma unroll
+				for (int h = 0; h < 7; h++)
+					if (Hm.mask & (1 << h)) use(Hm.ht[h], Hm.hm[h], Hm.w[h]);
+			}
+		};
+		V3 mc = v3(0, 0, 0), tc = v3(0, 0, 0);
+		if (translate) {
+			double wsum = 0;
+			each([&](V3 ht, V3 hm, double w) __attribute__((always_inline)) {
+				mc = mc + hm * (float)w;
+				tc = tc + ht * (float)w;
+				wsum += w;
+			});
+			if (wsum > 0) {
+				mc = divs(mc, (float)wsum);
+				tc = divs(tc, (float)wsum);
+			}
+			translation = tc - mc;
+		}
+		QSums S = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+		const V3 nmc = mc * -1.0f, ntc = tc * -1.0f;
+		each([&](V3 ht, V3 hm, double w) __attribute__((always_inline)) {
+			const V3 c1 = translate ? ht + ntc : ht, c2 = translate ? hm + nmc : hm;
+			qcp_accumulate(S, c1 * (float)w, c1, c2, w);
+		});
+		qrot = qcp_adjugate(S);
 	} else if (XS && xs) {
 		// Split-exchange (staging 4 / 5; m >= 2, several effectors): lane j of the group builds
 		// the headings of effectors e0+j, e0+j+m, ... with path sharing along its own sequence
@@ -1674,6 +1724,52 @@ __device__ __forceinline__ void global_pass(const DevPlan &t, int seg, const LV 
 	global_pass_pipelined(t, seg, L, G);
 }
 
+// Wave roles, cooperative segment (SCHED_XS): wave j of the segment's group of m waves walks the
+// paths of effectors e0+j, e0+j+m, ... from bone-step k's Gb -- the parent's iteration-start
+// global and the bone's local, exactly as bone_step forms them -- with path sharing along its own
+// sequence (the shared depth with a neighbour is the least over the effectors in between, as in
+// the split-exchange branch), and leaves each effector's bone-direction global E in the block's
+// exchange area xw: [slot][12 floats][64 lanes], slot = seg_hbase[seg] + i - e0.
+template <int TA, int PM, class LV, class GV, class FP, class IP>
+__device__ void coop_walk(const DevPlan &t, int seg, int k, int j, int m, size_t s, const LV &L, const GV &G, const FP TG,
+		const FP ST, const IP SF, float *xw) {
+	const int4 sr = t.step_rec[k];
+	const int b = sr.x & 0xffff;
+	const int flags = sr.z & 0xffff;
+	const int d0 = sr.z >> 16;
+	X3 P = xid();
+	if (flags & mbik::SR_PARENT_GLOBAL) {
+		P = G.ld((sr.y & 0xffff) - 1);
+		for (int q = (sr.x >> 16) - 2; q > k; q--) P = P * L.ld(t.seg_bones[q]);
+	}
+	const X3 Lb = L.ld(b);
+	const X3 Gb = (flags & mbik::SR_HAS_POSE_PARENT) ? P * Lb : Lb;
+	const int e0 = t.seg_eff_off[seg], e1 = t.seg_eff_off[seg + 1];
+	const double *hw = t.seg_hw + t.seg_hw_off[seg];
+	float *xe = xw + (size_t)t.seg_hbase[seg] * (12 * 64) + __lane_id();
+	PathCk pc;
+	pc.d = -1;
+	for (int i = e0 + j; i < e1; i += m) {
+		int lc[2] = {0, 0};
+		if (i - m >= e0) {
+			lc[0] = t.seg_eff_lcp[i];
+			for (int u = i - m + 1; u < i; u++) lc[0] = min(lc[0], t.seg_eff_lcp[u]);
+		}
+		if (i + m < e1) {
+			lc[1] = t.seg_eff_lcp[i + 1];
+			for (int u = i + 2; u <= i + m; u++) lc[1] = min(lc[1], t.seg_eff_lcp[u]);
+		}
+		X3 E;
+		Headings H; // (unused: the group's first wave builds the headings from E)
+		effector_headings<TA, PM>(t, t.seg_effs[i], d0, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, TG, 0, &pc, lc, &E);
+		float *r = xe + (size_t)(i - e0) * (12 * 64);
+		r[0] = E.b.r[0].x; r[64] = E.b.r[0].y; r[128] = E.b.r[0].z;
+		r[192] = E.b.r[1].x; r[256] = E.b.r[1].y; r[320] = E.b.r[1].z;
+		r[384] = E.b.r[2].x; r[448] = E.b.r[2].y; r[512] = E.b.r[2].z;
+		r[576] = E.o.x; r[640] = E.o.y; r[704] = E.o.z;
+	}
+}
+
 // IKBone3D::set_skeleton_bone_pose (ik_bone_3d.cpp:170-179); returns whether the basis was
 // non-finite (and replaced by the identity, :174-176).
 template <bool SEL = false>
@@ -1800,8 +1896,10 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 	constexpr int TA = PL == 2 ? kTabTiled : (T32 ? kTab32 : kTab64); // placement 2 reads the tiled table copy
 	const FP OE = rebind<float>(uplus(SF, P));    // stabilization only: 3 per pin
 	const FP MS = uplus(OE, 3 * P);              // stabilization only: 7 per pin
-	// wave roles: the block's 64 non-finite flags, after the topology (write_nonfinite)
+	// wave roles: the block's 64 non-finite flags after the topology (write_nonfinite), then the
+	// cooperative segments' effector-global exchange area (coop_walk)
 	int *nf_rw = RW ? reinterpret_cast<int *>(lds) : nullptr;
+	float *xw = RW ? lds + 64 : nullptr;
 	if constexpr (RW) {
 		if (threadIdx.x < 64) nf_rw[threadIdx.x] = 0;
 	}
@@ -1916,8 +2014,8 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 					if (rp) hrec = rp + (size_t)seq * kHelpF4 * 64;
 #endif
 					if (k0 + q < k1)
-						bone_step<false, true, kTab32, true, false, PM, true>(t, seg, k0 + q, task.y, task.z, task.w & mbik::SCHED_XS, s, L, G, TG, ST,
-								SF, HS, OE, MS, prev_dev, pre, hoist, hrec, b_ready ? nullptr : hfl, seq, &stuck MBIK_PROF_ARG);
+						bone_step<false, true, kTab32, true, false, PM, true, false>(t, seg, k0 + q, task.y, task.z, task.w & mbik::SCHED_XS, s, L, G, TG,
+								ST, SF, HS, OE, MS, prev_dev, pre, hoist, hrec, b_ready ? nullptr : hfl, seq, &stuck, nullptr MBIK_PROF_ARG);
 					help_post(hfl + 2, seq + 1);
 					slot = slot + 1 == kHelpSlots ? 0 : slot + 1;
 				}
@@ -1942,6 +2040,37 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 		MBIK_PROF_T(pg1);
 		MBIK_PROF_ADD(5, pg0, pg1);
 		for (int r = 0; r < t.nrows;) {
+			if constexpr (RW) {
+				if (t.sched[r * K].w & mbik::SCHED_COOP) {
+					// A row with cooperative segments: per bone-step, the groups' waves walk their
+					// effectors' paths (coop_walk) and meet; each group's first wave -- and each wave
+					// of a segment solved alone -- runs the step; the block meets again before the
+					// next step walks from the bones just solved.  Every wave runs the row's step
+					// count, so the barriers match.
+					const int4 task = t.sched[r * K + role];
+					const bool act = valid && task.x >= seg_lo && task.x <= seg_hi;
+					const int seg = task.x >= 0 ? task.x : 0;
+					const int k0 = t.seg_bone_off[seg], k1 = task.x >= 0 ? t.seg_bone_off[seg + 1] : k0;
+					const bool coop = (task.w & mbik::SCHED_XS) != 0;
+					const int nq = row_steps(t, r, seg_lo, seg_hi);
+					double prev_dev = INFINITY;
+					EffPre pre;
+					const int e0 = t.seg_eff_off[seg];
+					const bool hoist = HOIST && act && !coop && t.seg_eff_off[seg + 1] - e0 == 1;
+					if (hoist) load_eff<TA>(t, t.seg_effs[e0], TG, s, t.seg_hw + t.seg_hw_off[seg] + t.seg_eff_hoff[e0], pre);
+					for (int q = 0; q < nq; q++) {
+						const bool step = act && k0 + q < k1;
+						if (coop && step) coop_walk<TA, PM>(t, seg, k0 + q, task.y, task.z, s, L, G, TG, ST, SF, xw);
+						__syncthreads();
+						if (step && task.y == 0)
+							bone_step<false, true, TA, false, false, PM, HOIST, true>(t, seg, k0 + q, 0, 1, coop ? 1 : 0, s, L, G, TG, ST, SF,
+									HS, OE, MS, prev_dev, pre, hoist, nullptr, nullptr, 0, nullptr, xw MBIK_PROF_ARG);
+						__syncthreads();
+					}
+					r++;
+					continue;
+				}
+			}
 			// rows r .. r1-1: one row, or a packed level (SCHED_CHAIN rows, build_schedule) whose
 			// lanes each run their sequence of segments back to back, without a barrier
 			int r1 = r + 1;
@@ -1969,8 +2098,8 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 					}
 				}
 				if (k >= ke) break;
-				bone_step<STAB, HOIST || PL == 2, TA, false, XS, PM, HOIST>(t, seg, k, task.y, task.z, task.w & mbik::SCHED_XS, s, L, G, TG, ST, SF,
-						HS, OE, MS, prev_dev, pre, hoist, nullptr, nullptr, 0, nullptr MBIK_PROF_ARG);
+				bone_step<STAB, HOIST || PL == 2, TA, false, XS, PM, HOIST, false>(t, seg, k, task.y, task.z, task.w & mbik::SCHED_XS, s, L, G, TG,
+						ST, SF, HS, OE, MS, prev_dev, pre, hoist, nullptr, nullptr, 0, nullptr, nullptr MBIK_PROF_ARG);
 				k++;
 			}
 			__syncthreads();
@@ -2514,6 +2643,7 @@ int ensure_schedule(mbik_plan *p, int64_t nlaunch) {
 	p->dev.log2K = h.log2K;
 	p->dev.spw = h.spw;
 	p->dev.hs_floats = h.hs_floats;
+	p->dev.rw_xslots = h.rw_xslots;
 	p->dev.n_gck = h.n_gck;
 	p->dev.lds_stride = (mbik::lds_floats_per_skeleton(h) + 3) & ~3;
 	return MBIK_OK;
@@ -2751,7 +2881,8 @@ int launch(mbik_plan *p, int first, int count, const float *pose_in, const float
 	unsigned threads = 64;
 	if (h.wave_roles) {
 		threads = 64u * (unsigned)h.K; // a wave per role
-		lds += 64 * sizeof(int);      // the block's non-finite flags
+		lds += 64 * sizeof(int) + (size_t)h.rw_xslots * 12 * 64 * sizeof(float); // non-finite flags, effector-global exchange
+		if (lds > 160 * 1024) return fail(MBIK_EUNSUPPORTED, "wave roles: a row's effector-global exchange exceeds the LDS");
 	} else if (helper_on(p)) {
 		static std::once_flag honce;
 		std::call_once(honce, [] {
