@@ -1841,6 +1841,10 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 		uint4 *dst = reinterpret_cast<uint4 *>(lds4);
 		for (int i = (int)threadIdx.x; i < (t.topo_words >> 2); i += HELP ? 128 : RW ? 64 * RW : 64) dst[i] = t.topo_blob[i];
 	}
+	// several waves copied the blob: every wave reads all of it from here on (the pose load below
+	// reads bone_flags), so the copy must be complete -- a one-wave block's own LDS writes are
+	// ordered before its reads already
+	if constexpr (HELP || RW > 1) __syncthreads();
 	const uint32_t *topo = reinterpret_cast<const uint32_t *>(lds4);
 #define MBIK_REPOINT(T, name) t.name = reinterpret_cast<const T *>(topo + t.o_##name);
 	MBIK_TOPO_TABLES(MBIK_REPOINT)
