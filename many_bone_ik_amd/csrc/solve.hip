@@ -81,6 +81,7 @@ struct DevPlan {
 	int prio_mask = 0;   // kPrioDefault if every effector has that heading slot mask, else 0
 	int hs_floats;       // staged-heading LDS floats per skeleton
 	int rw_xslots = 0;   // wave roles: effector-global exchange slots (12 floats x 64 lanes of LDS each)
+	int rw_xsums = 0;    // wave roles: QCP-sum areas (11 doubles x 64 lanes each), after the slots
 	int n_gck;           // checkpoint globals per skeleton (HostPlan::bone_gslot)
 	int constraint_mode; // ManyBoneIK3D::constraint_mode
 	int libm;            // the reference host's glibc sinf/cosf build (gd::LIBM_FMA / LIBM_SSE2)
@@ -1044,7 +1045,7 @@ __device__ __forceinline__ void qcp_accumulate(QSums &S, const V3 wc1, const V3 
 template <bool STAB, bool PR, int TA, bool HELP, bool XS, int PM, bool SEL, bool XW, class LV, class GV, class FP, class IP>
 __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, int xs, size_t s, const LV &L, const GV &G, const FP TG,
 		const FP ST, const IP SF, const FP HS, const FP OE, const FP MS, double &prev_dev, const EffPre &pre, bool hoist,
-		const float4 *hrec, int *hfl, int hseq, bool *hstuck, const float *xw MBIK_PROF_PARAM) {
+		const float4 *hrec, int *hfl, int hseq, bool *hstuck, const float *xw, V3 xtr MBIK_PROF_PARAM) {
 	MBIK_PROF_T(pt0);
 #ifdef MBIK_PROF
 	uint64_t pt1 = pt0, pt3 = pt0;
@@ -1115,50 +1116,18 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, int xs
 		}
 		qrot = qcp_single<SEL>(mvd, tgt);
 	} else if (XW && xs) {
-		// Wave roles, cooperative segment: every effector's bone-direction global E comes from the
-		// block's exchange area, where the group's waves left it after walking its path from this
-		// step's Gb (coop_walk, the same products as effector_headings).  The headings are built
-		// from E in the reference's effector order and summed as the one-lane branch below does,
-		// so every sum rounds the same; a translating segment builds them twice, as
-		// weighted_superpose does (qcp.cpp:220-248).
-		const float *xe = xw + (size_t)t.seg_hbase[seg] * (12 * 64) + __lane_id();
-		auto each = [&](auto &&use) __attribute__((always_inline)) {
-			for (int i = e0; i < e1; i++) {
-				EffPre p;
-				load_eff<TA, PM, false>(t, t.seg_effs[i], TG, s, hw + t.seg_eff_hoff[i], p);
-				const float *r = xe + (size_t)(i - e0) * (12 * 64);
-				X3 E;
-				E.b.r[0] = v3(r[0], r[64], r[128]);
-				E.b.r[1] = v3(r[192], r[256], r[320]);
-				E.b.r[2] = v3(r[384], r[448], r[512]);
-				E.o = v3(r[576], r[640], r[704]);
-				Headings Hm;
-				heading_terms<PM>(p, E, E.o, Gb.o, Hm);
-#pragma unroll
-				for (int h = 0; h < 7; h++)
-					if (Hm.mask & (1 << h)) use(Hm.ht[h], Hm.hm[h], Hm.w[h]);
-			}
-		};
-		V3 mc = v3(0, 0, 0), tc = v3(0, 0, 0);
-		if (translate) {
-			double wsum = 0;
-			each([&](V3 ht, V3 hm, double w) __attribute__((always_inline)) {
-				mc = mc + hm * (float)w;
-				tc = tc + ht * (float)w;
-				wsum += w;
-			});
-			if (wsum > 0) {
-				mc = divs(mc, (float)wsum);
-				tc = divs(tc, (float)wsum);
-			}
-			translation = tc - mc;
-		}
-		QSums S = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-		const V3 nmc = mc * -1.0f, ntc = tc * -1.0f;
-		each([&](V3 ht, V3 hm, double w) __attribute__((always_inline)) {
-			const V3 c1 = translate ? ht + ntc : ht, c2 = translate ? hm + nmc : hm;
-			qcp_accumulate(S, c1 * (float)w, c1, c2, w);
-		});
+		// Wave roles, cooperative segment: the group's waves walked the effector paths and summed
+		// the headings (coop_walk, coop_sums: each of QCP::inner_product's eleven sums accumulated
+		// by one wave in the reference's heading order, as qcp_accumulate adds it); the sums and
+		// the centroid translation come in from the block's LDS.
+		const double *xs = reinterpret_cast<const double *>(xw + (size_t)t.rw_xslots * (12 * 64)) +
+				(size_t)(t.seg_hbase[seg] >> 16) * (11 * 64) + __lane_id();
+		QSums S;
+		S.xx = xs[0]; S.xy = xs[64]; S.xz = xs[128];
+		S.yx = xs[192]; S.yy = xs[256]; S.yz = xs[320];
+		S.zx = xs[384]; S.zy = xs[448]; S.zz = xs[512];
+		S.ss1 = xs[576]; S.ss2 = xs[640];
+		if (translate) translation = xtr;
 		qrot = qcp_adjugate(S);
 	} else if (XS && xs) {
 		// Split-exchange (staging 4 / 5; m >= 2, several effectors): lane j of the group builds
@@ -1731,7 +1700,7 @@ __device__ __forceinline__ void global_pass(const DevPlan &t, int seg, const LV 
 // the split-exchange branch), and leaves each effector's bone-direction global E in the block's
 // exchange area xw: [slot][12 floats][64 lanes], slot = seg_hbase[seg] + i - e0.
 template <int TA, int PM, class LV, class GV, class FP, class IP>
-__device__ void coop_walk(const DevPlan &t, int seg, int k, int j, int m, size_t s, const LV &L, const GV &G, const FP TG,
+__device__ X3 coop_walk(const DevPlan &t, int seg, int k, int j, int m, size_t s, const LV &L, const GV &G, const FP TG,
 		const FP ST, const IP SF, float *xw) {
 	const int4 sr = t.step_rec[k];
 	const int b = sr.x & 0xffff;
@@ -1768,6 +1737,87 @@ __device__ void coop_walk(const DevPlan &t, int seg, int k, int j, int m, size_t
 		r[384] = E.b.r[2].x; r[448] = E.b.r[2].y; r[512] = E.b.r[2].z;
 		r[576] = E.o.x; r[640] = E.o.y; r[704] = E.o.z;
 	}
+	return Gb;
+}
+
+// One term of QCP::inner_product's sum q (qcp.cpp:162-218) for a heading pair, as qcp_accumulate
+// forms it: q 0-8 the float products wc1_a * c2_b (a, b = x, y, z), 9 dot(wc1, c1), 10
+// w * dot(c2, c2), widened to double.  q is uniform over the wave.
+__device__ __forceinline__ double qcp_term(int q, V3 wc1, V3 c1, V3 c2, double w) {
+	switch (q) {
+	case 0: return (double)(c2.x * wc1.x);
+	case 1: return (double)(c2.y * wc1.x);
+	case 2: return (double)(wc1.x * c2.z);
+	case 3: return (double)(c2.x * wc1.y);
+	case 4: return (double)(c2.y * wc1.y);
+	case 5: return (double)(wc1.y * c2.z);
+	case 6: return (double)(c2.x * wc1.z);
+	case 7: return (double)(c2.y * wc1.z);
+	case 8: return (double)(wc1.z * c2.z);
+	case 9: return (double)dot(wc1, c1);
+	default: return w * (double)dot(c2, c2);
+	}
+}
+
+// Wave roles, cooperative segment, after coop_walk's barrier: every wave j of the group builds
+// every heading from the effector globals in LDS -- in the reference's effector order, with the
+// centroids of QCP::move_to_weighted_center for a translating segment (qcp.cpp:139-160, float
+// sums and a double weight sum, as bone_step's one-lane branch forms them) -- and accumulates the
+// inner-product sums q = j, j + m, ... (< 11), each in heading order as qcp_accumulate adds it, so
+// every sum rounds as the reference's loop does; it leaves them in the segment's sum area.
+// Returns the translation (target centre - moved centre).
+template <int TA, int PM, class FP>
+__device__ V3 coop_sums(const DevPlan &t, int seg, int j, int m, const X3 &Gb, const FP TG, size_t s, float *xw) {
+	const int e0 = t.seg_eff_off[seg], e1 = t.seg_eff_off[seg + 1];
+	const bool translate = (t.seg_flags[seg] & mbik::SF_TRANSLATE) != 0;
+	const double *hw = t.seg_hw + t.seg_hw_off[seg];
+	const float *xe = xw + (size_t)(t.seg_hbase[seg] & 0xffff) * (12 * 64) + __lane_id();
+	double *xs = reinterpret_cast<double *>(xw + (size_t)t.rw_xslots * (12 * 64)) + (size_t)(t.seg_hbase[seg] >> 16) * (11 * 64) +
+			__lane_id();
+	auto each = [&](auto &&use) __attribute__((always_inline)) {
+		for (int i = e0; i < e1; i++) {
+			EffPre p;
+			load_eff<TA, PM, false>(t, t.seg_effs[i], TG, s, hw + t.seg_eff_hoff[i], p);
+			const float *r = xe + (size_t)(i - e0) * (12 * 64);
+			X3 E;
+			E.b.r[0] = v3(r[0], r[64], r[128]);
+			E.b.r[1] = v3(r[192], r[256], r[320]);
+			E.b.r[2] = v3(r[384], r[448], r[512]);
+			E.o = v3(r[576], r[640], r[704]);
+			Headings Hm;
+			heading_terms<PM>(p, E, E.o, Gb.o, Hm);
+#pragma unroll
+			for (int h = 0; h < 7; h++)
+				if (Hm.mask & (1 << h)) use(Hm.ht[h], Hm.hm[h], Hm.w[h]);
+		}
+	};
+	V3 mc = v3(0, 0, 0), tc = v3(0, 0, 0);
+	if (translate) {
+		double wsum = 0;
+		each([&](V3 ht, V3 hm, double w) __attribute__((always_inline)) {
+			mc = mc + hm * (float)w;
+			tc = tc + ht * (float)w;
+			wsum += w;
+		});
+		if (wsum > 0) {
+			mc = divs(mc, (float)wsum);
+			tc = divs(tc, (float)wsum);
+		}
+	}
+	const V3 nmc = mc * -1.0f, ntc = tc * -1.0f;
+	// this wave's sums: q = j + u * m, u < 6 (m >= 2)
+	double a[6] = {0, 0, 0, 0, 0, 0};
+	each([&](V3 ht, V3 hm, double w) __attribute__((always_inline)) {
+		const V3 c1 = translate ? ht + ntc : ht, c2 = translate ? hm + nmc : hm;
+		const V3 wc1 = c1 * (float)w;
+#pragma unroll
+		for (int u = 0; u < 6; u++)
+			if (j + u * m < 11) a[u] += qcp_term(j + u * m, wc1, c1, c2, w);
+	});
+#pragma unroll
+	for (int u = 0; u < 6; u++)
+		if (j + u * m < 11) xs[(j + u * m) * 64] = a[u];
+	return tc - mc;
 }
 
 // IKBone3D::set_skeleton_bone_pose (ik_bone_3d.cpp:170-179); returns whether the basis was
@@ -2019,7 +2069,7 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 #endif
 					if (k0 + q < k1)
 						bone_step<false, true, kTab32, true, false, PM, true, false>(t, seg, k0 + q, task.y, task.z, task.w & mbik::SCHED_XS, s, L, G, TG,
-								ST, SF, HS, OE, MS, prev_dev, pre, hoist, hrec, b_ready ? nullptr : hfl, seq, &stuck, nullptr MBIK_PROF_ARG);
+								ST, SF, HS, OE, MS, prev_dev, pre, hoist, hrec, b_ready ? nullptr : hfl, seq, &stuck, nullptr, V3{} MBIK_PROF_ARG);
 					help_post(hfl + 2, seq + 1);
 					slot = slot + 1 == kHelpSlots ? 0 : slot + 1;
 				}
@@ -2064,11 +2114,15 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 					if (hoist) load_eff<TA>(t, t.seg_effs[e0], TG, s, t.seg_hw + t.seg_hw_off[seg] + t.seg_eff_hoff[e0], pre);
 					for (int q = 0; q < nq; q++) {
 						const bool step = act && k0 + q < k1;
-						if (coop && step) coop_walk<TA, PM>(t, seg, k0 + q, task.y, task.z, s, L, G, TG, ST, SF, xw);
+						X3 Gb;
+						if (coop && step) Gb = coop_walk<TA, PM>(t, seg, k0 + q, task.y, task.z, s, L, G, TG, ST, SF, xw);
+						__syncthreads();
+						V3 tr = v3(0, 0, 0);
+						if (coop && step) tr = coop_sums<TA, PM>(t, seg, task.y, task.z, Gb, TG, s, xw);
 						__syncthreads();
 						if (step && task.y == 0)
 							bone_step<false, true, TA, false, false, PM, HOIST, true>(t, seg, k0 + q, 0, 1, coop ? 1 : 0, s, L, G, TG, ST, SF,
-									HS, OE, MS, prev_dev, pre, hoist, nullptr, nullptr, 0, nullptr, xw MBIK_PROF_ARG);
+									HS, OE, MS, prev_dev, pre, hoist, nullptr, nullptr, 0, nullptr, xw, tr MBIK_PROF_ARG);
 						__syncthreads();
 					}
 					r++;
@@ -2103,7 +2157,7 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 				}
 				if (k >= ke) break;
 				bone_step<STAB, HOIST || PL == 2, TA, false, XS, PM, HOIST, false>(t, seg, k, task.y, task.z, task.w & mbik::SCHED_XS, s, L, G, TG,
-						ST, SF, HS, OE, MS, prev_dev, pre, hoist, nullptr, nullptr, 0, nullptr, nullptr MBIK_PROF_ARG);
+						ST, SF, HS, OE, MS, prev_dev, pre, hoist, nullptr, nullptr, 0, nullptr, nullptr, V3{} MBIK_PROF_ARG);
 				k++;
 			}
 			__syncthreads();
@@ -2648,6 +2702,7 @@ int ensure_schedule(mbik_plan *p, int64_t nlaunch) {
 	p->dev.spw = h.spw;
 	p->dev.hs_floats = h.hs_floats;
 	p->dev.rw_xslots = h.rw_xslots;
+	p->dev.rw_xsums = h.rw_xsums;
 	p->dev.n_gck = h.n_gck;
 	p->dev.lds_stride = (mbik::lds_floats_per_skeleton(h) + 3) & ~3;
 	return MBIK_OK;
@@ -2885,7 +2940,8 @@ int launch(mbik_plan *p, int first, int count, const float *pose_in, const float
 	unsigned threads = 64;
 	if (h.wave_roles) {
 		threads = 64u * (unsigned)h.K; // a wave per role
-		lds += 64 * sizeof(int) + (size_t)h.rw_xslots * 12 * 64 * sizeof(float); // non-finite flags, effector-global exchange
+		// non-finite flags, effector-global exchange, QCP-sum areas
+		lds += 64 * sizeof(int) + (size_t)h.rw_xslots * 12 * 64 * sizeof(float) + (size_t)h.rw_xsums * 11 * 64 * sizeof(double);
 		if (lds > 160 * 1024) return fail(MBIK_EUNSUPPORTED, "wave roles: a row's effector-global exchange exceeds the LDS");
 	} else if (helper_on(p)) {
 		static std::once_flag honce;
