@@ -1715,7 +1715,7 @@ __device__ X3 coop_walk(const DevPlan &t, int seg, int k, int j, int m, size_t s
 	const X3 Gb = (flags & mbik::SR_HAS_POSE_PARENT) ? P * Lb : Lb;
 	const int e0 = t.seg_eff_off[seg], e1 = t.seg_eff_off[seg + 1];
 	const double *hw = t.seg_hw + t.seg_hw_off[seg];
-	float *xe = xw + (size_t)t.seg_hbase[seg] * (12 * 64) + __lane_id();
+	float *xe = xw + (size_t)(t.seg_hbase[seg] & 0xffff) * (12 * 64) + __lane_id();
 	PathCk pc;
 	pc.d = -1;
 	for (int i = e0 + j; i < e1; i += m) {
