@@ -1740,31 +1740,13 @@ __device__ X3 coop_walk(const DevPlan &t, int seg, int k, int j, int m, size_t s
 	return Gb;
 }
 
-// One term of QCP::inner_product's sum q (qcp.cpp:162-218) for a heading pair, as qcp_accumulate
-// forms it: q 0-8 the float products wc1_a * c2_b (a, b = x, y, z), 9 dot(wc1, c1), 10
-// w * dot(c2, c2), widened to double.  q is uniform over the wave.
-__device__ __forceinline__ double qcp_term(int q, V3 wc1, V3 c1, V3 c2, double w) {
-	switch (q) {
-	case 0: return (double)(c2.x * wc1.x);
-	case 1: return (double)(c2.y * wc1.x);
-	case 2: return (double)(wc1.x * c2.z);
-	case 3: return (double)(c2.x * wc1.y);
-	case 4: return (double)(c2.y * wc1.y);
-	case 5: return (double)(wc1.y * c2.z);
-	case 6: return (double)(c2.x * wc1.z);
-	case 7: return (double)(c2.y * wc1.z);
-	case 8: return (double)(wc1.z * c2.z);
-	case 9: return (double)dot(wc1, c1);
-	default: return w * (double)dot(c2, c2);
-	}
-}
-
 // Wave roles, cooperative segment, after coop_walk's barrier: every wave j of the group builds
 // every heading from the effector globals in LDS -- in the reference's effector order, with the
 // centroids of QCP::move_to_weighted_center for a translating segment (qcp.cpp:139-160, float
 // sums and a double weight sum, as bone_step's one-lane branch forms them) -- and accumulates the
-// inner-product sums q = j, j + m, ... (< 11), each in heading order as qcp_accumulate adds it, so
-// every sum rounds as the reference's loop does; it leaves them in the segment's sum area.
+// inner-product sums of its share (four groups of them over the first waves), each in heading
+// order as qcp_accumulate adds it, so every sum rounds as the reference's loop does; it leaves
+// them in the segment's sum area.
 // Returns the translation (target centre - moved centre).
 template <int TA, int PM, class FP>
 __device__ V3 coop_sums(const DevPlan &t, int seg, int j, int m, const X3 &Gb, const FP TG, size_t s, float *xw) {
@@ -1805,18 +1787,40 @@ __device__ V3 coop_sums(const DevPlan &t, int seg, int j, int m, const X3 &Gb, c
 		}
 	}
 	const V3 nmc = mc * -1.0f, ntc = tc * -1.0f;
-	// this wave's sums: q = j + u * m, u < 6 (m >= 2)
-	double a[6] = {0, 0, 0, 0, 0, 0};
-	each([&](V3 ht, V3 hm, double w) __attribute__((always_inline)) {
-		const V3 c1 = translate ? ht + ntc : ht, c2 = translate ? hm + nmc : hm;
-		const V3 wc1 = c1 * (float)w;
-#pragma unroll
-		for (int u = 0; u < 6; u++)
-			if (j + u * m < 11) a[u] += qcp_term(j + u * m, wc1, c1, c2, w);
-	});
-#pragma unroll
-	for (int u = 0; u < 6; u++)
-		if (j + u * m < 11) xs[(j + u * m) * 64] = a[u];
+	// This wave's sums, in four groups: xx xy xz | yx yy yz | zx zy zz | ss1 ss2.  Two waves take
+	// two groups each, four or more one group each (waves past the fourth sum nothing); the group
+	// tests are uniform over the wave.
+	const int gm = m == 2 ? (j == 0 ? 3 : 12) : (j < 4 ? 1 << j : 0);
+	double a0 = 0, a1 = 0, a2 = 0, a3 = 0, a4 = 0, a5 = 0, a6 = 0, a7 = 0, a8 = 0, a9 = 0, a10 = 0;
+	if (gm)
+		each([&](V3 ht, V3 hm, double w) __attribute__((always_inline)) {
+			const V3 c1 = translate ? ht + ntc : ht, c2 = translate ? hm + nmc : hm;
+			const V3 wc1 = c1 * (float)w;
+			// the float products as qcp_accumulate forms them (each the scalar IEEE product)
+			if (gm & 1) {
+				a0 += (double)(c2.x * wc1.x);
+				a1 += (double)(c2.y * wc1.x);
+				a2 += (double)(wc1.x * c2.z);
+			}
+			if (gm & 2) {
+				a3 += (double)(c2.x * wc1.y);
+				a4 += (double)(c2.y * wc1.y);
+				a5 += (double)(wc1.y * c2.z);
+			}
+			if (gm & 4) {
+				a6 += (double)(c2.x * wc1.z);
+				a7 += (double)(c2.y * wc1.z);
+				a8 += (double)(wc1.z * c2.z);
+			}
+			if (gm & 8) {
+				a9 += (double)dot(wc1, c1);
+				a10 += w * (double)dot(c2, c2);
+			}
+		});
+	if (gm & 1) { xs[0] = a0; xs[64] = a1; xs[128] = a2; }
+	if (gm & 2) { xs[192] = a3; xs[256] = a4; xs[320] = a5; }
+	if (gm & 4) { xs[384] = a6; xs[448] = a7; xs[512] = a8; }
+	if (gm & 8) { xs[576] = a9; xs[640] = a10; }
 	return tc - mc;
 }
 
