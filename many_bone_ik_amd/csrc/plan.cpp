@@ -721,22 +721,18 @@ void build_schedule(HostPlan &p, int32_t lanes, int64_t nlaunch, int32_t spw_ove
 	p.seg_hbase.assign(p.NS, 0);
 	p.hs_floats = 0;
 	p.rw_xslots = 0;
-	p.rw_xsums = 0;
 	if (p.wave_roles) {
 		// wave roles: a cooperative segment's effector globals go through LDS, one slot per
-		// effector, and so do its QCP sums, one area per segment; the segments of a row run
-		// concurrently, so their slots and areas are disjoint
+		// effector; the segments of a row run concurrently, so their slots are disjoint
 		for (int r = 0; r < p.nrows; r++) {
-			int used = 0, sums = 0;
+			int used = 0;
 			for (int l = 0; l < K; l++) {
 				const SchedTask &tk = p.sched[(size_t)r * K + l];
 				if (tk.seg < 0 || tk.j != 0 || !(tk.flags & SCHED_XS)) continue;
-				p.seg_hbase[tk.seg] = used | (sums << 16);
+				p.seg_hbase[tk.seg] = used;
 				used += p.seg_eff_off[tk.seg + 1] - p.seg_eff_off[tk.seg];
-				sums++;
 			}
 			p.rw_xslots = std::max(p.rw_xslots, used);
-			p.rw_xsums = std::max(p.rw_xsums, sums);
 		}
 	}
 	for (int r = 0; r < p.nrows && !p.wave_roles; r++) {
@@ -847,7 +843,7 @@ void build_schedule(HostPlan &p, int32_t lanes, int64_t nlaunch, int32_t spw_ove
 	}
 	p.spw = best;
 	p.lds_block_bytes = best * (int64_t)(((lds_floats_per_skeleton(p) + 3) & ~3) * 4) + topo +
-			(p.wave_roles ? 64 * 4 + (int64_t)p.rw_xslots * 12 * 64 * 4 + (int64_t)p.rw_xsums * 11 * 64 * 8 : 0);
+			(p.wave_roles ? 64 * 4 + (p.rw_xslots ? ((int64_t)p.P + p.rw_xslots) * 12 * 64 * 4 : 0) : 0);
 }
 
 } // namespace mbik

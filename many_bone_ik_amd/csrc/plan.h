@@ -133,10 +133,8 @@ struct HostPlan {
 	// another's work.  Whole state in device memory (state_hbm 2).  0: roles are lanes of a wave.
 	int32_t wave_roles = 0;
 	// wave roles: effector-global exchange slots of the cooperative rows (SCHED_COOP), the most any
-	// row needs (a slot is 12 floats x 64 lanes of LDS), and QCP-sum areas (one per cooperative
-	// segment of a row: 11 doubles x 64 lanes).  seg_hbase[seg] = the segment's first slot | its
-	// sum area << 16.
-	int32_t rw_xslots = 0, rw_xsums = 0;
+	// row needs; a slot is 12 floats x 64 lanes of LDS.  seg_hbase[seg] is the segment's first slot.
+	int32_t rw_xslots = 0;
 	// Iteration-start globals kept in LDS only for checkpoint bones: every g_interval-th bone
 	// of a segment counted from its root (the root included) and every parent of a segment
 	// root; a bone-step rebuilds its parent's global from the nearest checkpoint above it.

@@ -81,7 +81,6 @@ struct DevPlan {
 	int prio_mask = 0;   // kPrioDefault if every effector has that heading slot mask, else 0
 	int hs_floats;       // staged-heading LDS floats per skeleton
 	int rw_xslots = 0;   // wave roles: effector-global exchange slots (12 floats x 64 lanes of LDS each)
-	int rw_xsums = 0;    // wave roles: QCP-sum areas (11 doubles x 64 lanes each), after the slots
 	int n_gck;           // checkpoint globals per skeleton (HostPlan::bone_gslot)
 	int constraint_mode; // ManyBoneIK3D::constraint_mode
 	int libm;            // the reference host's glibc sinf/cosf build (gd::LIBM_FMA / LIBM_SSE2)
@@ -516,13 +515,11 @@ __device__ __forceinline__ bool prio_on(float pr, int a) {
 	else return pr > 0.0f;
 }
 // DB false: without the effector bone's bone-direction basis (only a path walk reads it).
-template <int TA, int PM = 0, bool DB = true, class FP>
-__device__ __forceinline__ void load_eff(const DevPlan &t, int e, const FP TG, size_t s, const double *hw, EffPre &p) {
+// The priorities and the slot-ordered QCP heading weights of effector e (the part of load_eff
+// that is topology, not per-skeleton state).
+template <int PM = 0>
+__device__ __forceinline__ void eff_weights(const DevPlan &t, int e, const double *hw, EffPre &p) {
 	p.e = e;
-	p.off = t.eff_path_off[e];
-	p.de = t.eff_path_off[e + 1] - p.off - 1;
-	p.T = ld_x(TG + 12 * e);
-	if constexpr (DB) p.Db = ld_soa_basis<TA>(t, t.D, t.eff_bone[e], 9, 0, s);
 	p.hws[0] = hw[0];
 	int k = 1;
 #pragma unroll
@@ -533,6 +530,24 @@ __device__ __forceinline__ void load_eff(const DevPlan &t, int e, const FP TG, s
 		p.hws[2 + 2 * a] = on ? hw[k + 1] : 0.0;
 		k += on ? 2 : 0;
 	}
+}
+template <int TA, int PM = 0, bool DB = true, class FP>
+__device__ __forceinline__ void load_eff(const DevPlan &t, int e, const FP TG, size_t s, const double *hw, EffPre &p) {
+	p.off = t.eff_path_off[e];
+	p.de = t.eff_path_off[e + 1] - p.off - 1;
+	p.T = ld_x(TG + 12 * e);
+	if constexpr (DB) p.Db = ld_soa_basis<TA>(t, t.D, t.eff_bone[e], 9, 0, s);
+	eff_weights<PM>(t, e, hw, p);
+}
+// A transform stored field-major over a wave's lanes (wave-roles LDS areas: [12][64], basis rows
+// then origin; p points at the lane's field 0).
+__device__ __forceinline__ X3 ld_x64(const float *r) {
+	X3 x;
+	x.b.r[0] = v3(r[0], r[64], r[128]);
+	x.b.r[1] = v3(r[192], r[256], r[320]);
+	x.b.r[2] = v3(r[384], r[448], r[512]);
+	x.o = v3(r[576], r[640], r[704]);
+	return x;
 }
 template <int PM = 0>
 __device__ __forceinline__ void heading_terms(const EffPre &p, const X3 &E, V3 oe, V3 ob, Headings &H);
@@ -1045,7 +1060,7 @@ __device__ __forceinline__ void qcp_accumulate(QSums &S, const V3 wc1, const V3 
 template <bool STAB, bool PR, int TA, bool HELP, bool XS, int PM, bool SEL, bool XW, class LV, class GV, class FP, class IP>
 __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, int xs, size_t s, const LV &L, const GV &G, const FP TG,
 		const FP ST, const IP SF, const FP HS, const FP OE, const FP MS, double &prev_dev, const EffPre &pre, bool hoist,
-		const float4 *hrec, int *hfl, int hseq, bool *hstuck, const float *xw, V3 xtr MBIK_PROF_PARAM) {
+		const float4 *hrec, int *hfl, int hseq, bool *hstuck, const float *xw MBIK_PROF_PARAM) {
 	MBIK_PROF_T(pt0);
 #ifdef MBIK_PROF
 	uint64_t pt1 = pt0, pt3 = pt0;
@@ -1116,18 +1131,49 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, int xs
 		}
 		qrot = qcp_single<SEL>(mvd, tgt);
 	} else if (XW && xs) {
-		// Wave roles, cooperative segment: the group's waves walked the effector paths and summed
-		// the headings (coop_walk, coop_sums: each of QCP::inner_product's eleven sums accumulated
-		// by one wave in the reference's heading order, as qcp_accumulate adds it); the sums and
-		// the centroid translation come in from the block's LDS.
-		const double *xs = reinterpret_cast<const double *>(xw + (size_t)t.rw_xslots * (12 * 64)) +
-				(size_t)(t.seg_hbase[seg] >> 16) * (11 * 64) + __lane_id();
-		QSums S;
-		S.xx = xs[0]; S.xy = xs[64]; S.xz = xs[128];
-		S.yx = xs[192]; S.yy = xs[256]; S.yz = xs[320];
-		S.zx = xs[384]; S.zy = xs[448]; S.zz = xs[512];
-		S.ss1 = xs[576]; S.ss2 = xs[640];
-		if (translate) translation = xtr;
+		// Wave roles, cooperative segment: every effector's bone-direction global E comes from the
+		// block's exchange area, where the group's waves left it after walking its path from this
+		// step's Gb (coop_walk, the same products as effector_headings).  The headings are built
+		// from E in the reference's effector order and summed as the one-lane branch below does,
+		// so every sum rounds the same; a translating segment builds them twice, as
+		// weighted_superpose does (qcp.cpp:220-248).
+		// (the block's copy of the targets precedes the exchange area: [pin][12][64 lanes])
+		const float *xe = xw + (size_t)t.seg_hbase[seg] * (12 * 64) + __lane_id();
+		const float *xt = xw - (size_t)t.P * (12 * 64) + __lane_id();
+		auto each = [&](auto &&use) __attribute__((always_inline)) {
+			for (int i = e0; i < e1; i++) {
+				const int e = t.seg_effs[i];
+				EffPre p;
+				eff_weights<PM>(t, e, hw + t.seg_eff_hoff[i], p);
+				p.T = ld_x64(xt + (size_t)e * (12 * 64));
+				const X3 E = ld_x64(xe + (size_t)(i - e0) * (12 * 64));
+				Headings Hm;
+				heading_terms<PM>(p, E, E.o, Gb.o, Hm);
+#pragma unroll
+				for (int h = 0; h < 7; h++)
+					if (Hm.mask & (1 << h)) use(Hm.ht[h], Hm.hm[h], Hm.w[h]);
+			}
+		};
+		V3 mc = v3(0, 0, 0), tc = v3(0, 0, 0);
+		if (translate) {
+			double wsum = 0;
+			each([&](V3 ht, V3 hm, double w) __attribute__((always_inline)) {
+				mc = mc + hm * (float)w;
+				tc = tc + ht * (float)w;
+				wsum += w;
+			});
+			if (wsum > 0) {
+				mc = divs(mc, (float)wsum);
+				tc = divs(tc, (float)wsum);
+			}
+			translation = tc - mc;
+		}
+		QSums S = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+		const V3 nmc = mc * -1.0f, ntc = tc * -1.0f;
+		each([&](V3 ht, V3 hm, double w) __attribute__((always_inline)) {
+			const V3 c1 = translate ? ht + ntc : ht, c2 = translate ? hm + nmc : hm;
+			qcp_accumulate(S, c1 * (float)w, c1, c2, w);
+		});
 		qrot = qcp_adjugate(S);
 	} else if (XS && xs) {
 		// Split-exchange (staging 4 / 5; m >= 2, several effectors): lane j of the group builds
@@ -1700,7 +1746,7 @@ __device__ __forceinline__ void global_pass(const DevPlan &t, int seg, const LV 
 // the split-exchange branch), and leaves each effector's bone-direction global E in the block's
 // exchange area xw: [slot][12 floats][64 lanes], slot = seg_hbase[seg] + i - e0.
 template <int TA, int PM, class LV, class GV, class FP, class IP>
-__device__ X3 coop_walk(const DevPlan &t, int seg, int k, int j, int m, size_t s, const LV &L, const GV &G, const FP TG,
+__device__ void coop_walk(const DevPlan &t, int seg, int k, int j, int m, size_t s, const LV &L, const GV &G, const FP TG,
 		const FP ST, const IP SF, float *xw) {
 	const int4 sr = t.step_rec[k];
 	const int b = sr.x & 0xffff;
@@ -1715,7 +1761,7 @@ __device__ X3 coop_walk(const DevPlan &t, int seg, int k, int j, int m, size_t s
 	const X3 Gb = (flags & mbik::SR_HAS_POSE_PARENT) ? P * Lb : Lb;
 	const int e0 = t.seg_eff_off[seg], e1 = t.seg_eff_off[seg + 1];
 	const double *hw = t.seg_hw + t.seg_hw_off[seg];
-	float *xe = xw + (size_t)(t.seg_hbase[seg] & 0xffff) * (12 * 64) + __lane_id();
+	float *xe = xw + (size_t)t.seg_hbase[seg] * (12 * 64) + __lane_id();
 	PathCk pc;
 	pc.d = -1;
 	for (int i = e0 + j; i < e1; i += m) {
@@ -1737,91 +1783,6 @@ __device__ X3 coop_walk(const DevPlan &t, int seg, int k, int j, int m, size_t s
 		r[384] = E.b.r[2].x; r[448] = E.b.r[2].y; r[512] = E.b.r[2].z;
 		r[576] = E.o.x; r[640] = E.o.y; r[704] = E.o.z;
 	}
-	return Gb;
-}
-
-// Wave roles, cooperative segment, after coop_walk's barrier: every wave j of the group builds
-// every heading from the effector globals in LDS -- in the reference's effector order, with the
-// centroids of QCP::move_to_weighted_center for a translating segment (qcp.cpp:139-160, float
-// sums and a double weight sum, as bone_step's one-lane branch forms them) -- and accumulates the
-// inner-product sums of its share (four groups of them over the first waves), each in heading
-// order as qcp_accumulate adds it, so every sum rounds as the reference's loop does; it leaves
-// them in the segment's sum area.
-// Returns the translation (target centre - moved centre).
-template <int TA, int PM, class FP>
-__device__ V3 coop_sums(const DevPlan &t, int seg, int j, int m, const X3 &Gb, const FP TG, size_t s, float *xw) {
-	const int e0 = t.seg_eff_off[seg], e1 = t.seg_eff_off[seg + 1];
-	const bool translate = (t.seg_flags[seg] & mbik::SF_TRANSLATE) != 0;
-	const double *hw = t.seg_hw + t.seg_hw_off[seg];
-	const float *xe = xw + (size_t)(t.seg_hbase[seg] & 0xffff) * (12 * 64) + __lane_id();
-	double *xs = reinterpret_cast<double *>(xw + (size_t)t.rw_xslots * (12 * 64)) + (size_t)(t.seg_hbase[seg] >> 16) * (11 * 64) +
-			__lane_id();
-	auto each = [&](auto &&use) __attribute__((always_inline)) {
-		for (int i = e0; i < e1; i++) {
-			EffPre p;
-			load_eff<TA, PM, false>(t, t.seg_effs[i], TG, s, hw + t.seg_eff_hoff[i], p);
-			const float *r = xe + (size_t)(i - e0) * (12 * 64);
-			X3 E;
-			E.b.r[0] = v3(r[0], r[64], r[128]);
-			E.b.r[1] = v3(r[192], r[256], r[320]);
-			E.b.r[2] = v3(r[384], r[448], r[512]);
-			E.o = v3(r[576], r[640], r[704]);
-			Headings Hm;
-			heading_terms<PM>(p, E, E.o, Gb.o, Hm);
-#pragma unroll
-			for (int h = 0; h < 7; h++)
-				if (Hm.mask & (1 << h)) use(Hm.ht[h], Hm.hm[h], Hm.w[h]);
-		}
-	};
-	V3 mc = v3(0, 0, 0), tc = v3(0, 0, 0);
-	if (translate) {
-		double wsum = 0;
-		each([&](V3 ht, V3 hm, double w) __attribute__((always_inline)) {
-			mc = mc + hm * (float)w;
-			tc = tc + ht * (float)w;
-			wsum += w;
-		});
-		if (wsum > 0) {
-			mc = divs(mc, (float)wsum);
-			tc = divs(tc, (float)wsum);
-		}
-	}
-	const V3 nmc = mc * -1.0f, ntc = tc * -1.0f;
-	// This wave's sums, in four groups: xx xy xz | yx yy yz | zx zy zz | ss1 ss2.  Two waves take
-	// two groups each, four or more one group each (waves past the fourth sum nothing); the group
-	// tests are uniform over the wave.
-	const int gm = m == 2 ? (j == 0 ? 3 : 12) : (j < 4 ? 1 << j : 0);
-	double a0 = 0, a1 = 0, a2 = 0, a3 = 0, a4 = 0, a5 = 0, a6 = 0, a7 = 0, a8 = 0, a9 = 0, a10 = 0;
-	if (gm)
-		each([&](V3 ht, V3 hm, double w) __attribute__((always_inline)) {
-			const V3 c1 = translate ? ht + ntc : ht, c2 = translate ? hm + nmc : hm;
-			const V3 wc1 = c1 * (float)w;
-			// the float products as qcp_accumulate forms them (each the scalar IEEE product)
-			if (gm & 1) {
-				a0 += (double)(c2.x * wc1.x);
-				a1 += (double)(c2.y * wc1.x);
-				a2 += (double)(wc1.x * c2.z);
-			}
-			if (gm & 2) {
-				a3 += (double)(c2.x * wc1.y);
-				a4 += (double)(c2.y * wc1.y);
-				a5 += (double)(wc1.y * c2.z);
-			}
-			if (gm & 4) {
-				a6 += (double)(c2.x * wc1.z);
-				a7 += (double)(c2.y * wc1.z);
-				a8 += (double)(wc1.z * c2.z);
-			}
-			if (gm & 8) {
-				a9 += (double)dot(wc1, c1);
-				a10 += w * (double)dot(c2, c2);
-			}
-		});
-	if (gm & 1) { xs[0] = a0; xs[64] = a1; xs[128] = a2; }
-	if (gm & 2) { xs[192] = a3; xs[256] = a4; xs[320] = a5; }
-	if (gm & 4) { xs[384] = a6; xs[448] = a7; xs[512] = a8; }
-	if (gm & 8) { xs[576] = a9; xs[640] = a10; }
-	return tc - mc;
 }
 
 // IKBone3D::set_skeleton_bone_pose (ik_bone_3d.cpp:170-179); returns whether the basis was
@@ -1957,7 +1918,10 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 	// wave roles: the block's 64 non-finite flags after the topology (write_nonfinite), then the
 	// cooperative segments' effector-global exchange area (coop_walk)
 	int *nf_rw = RW ? reinterpret_cast<int *>(lds) : nullptr;
-	float *xw = RW ? lds + 64 : nullptr;
+	// (a plan with cooperative rows keeps the block's targets in LDS too, [pin][12][64], before
+	// the exchange area: the cooperative consumer reads them for every effector at every step)
+	float *xt = RW ? lds + 64 : nullptr;
+	float *xw = RW ? xt + (t.rw_xslots ? (size_t)t.P * (12 * 64) : 0) : nullptr;
 	if constexpr (RW) {
 		if (threadIdx.x < 64) nf_rw[threadIdx.x] = 0;
 	}
@@ -1967,6 +1931,9 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 		for (int e = role; e < P; e += K) {
 			const float *src = targets + ((size_t)local * P + e) * 12;
 			for (int f = 0; f < 12; f++) TG[12 * e + f] = src[f];
+			if constexpr (RW > 0)
+				if (t.rw_xslots)
+					for (int f = 0; f < 12; f++) xt[((size_t)e * 12 + f) * 64 + lane] = src[f];
 			SF[e] = 0;
 		}
 	}
@@ -2073,7 +2040,7 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 #endif
 					if (k0 + q < k1)
 						bone_step<false, true, kTab32, true, false, PM, true, false>(t, seg, k0 + q, task.y, task.z, task.w & mbik::SCHED_XS, s, L, G, TG,
-								ST, SF, HS, OE, MS, prev_dev, pre, hoist, hrec, b_ready ? nullptr : hfl, seq, &stuck, nullptr, V3{} MBIK_PROF_ARG);
+								ST, SF, HS, OE, MS, prev_dev, pre, hoist, hrec, b_ready ? nullptr : hfl, seq, &stuck, nullptr MBIK_PROF_ARG);
 					help_post(hfl + 2, seq + 1);
 					slot = slot + 1 == kHelpSlots ? 0 : slot + 1;
 				}
@@ -2116,23 +2083,34 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 					const int e0 = t.seg_eff_off[seg];
 					const bool hoist = HOIST && act && !coop && t.seg_eff_off[seg + 1] - e0 == 1;
 					if (hoist) load_eff<TA>(t, t.seg_effs[e0], TG, s, t.seg_hw + t.seg_hw_off[seg] + t.seg_eff_hoff[e0], pre);
+					// (MBIK_PROF, wave roles: 18 packed / plain rows, 19 coop_walk, 21 waiting at the
+					// cooperative rows' barriers, 22 the steps run after them, 23 cooperative rows)
+					MBIK_PROF_T(cr0);
 					for (int q = 0; q < nq; q++) {
 						const bool step = act && k0 + q < k1;
-						X3 Gb;
-						if (coop && step) Gb = coop_walk<TA, PM>(t, seg, k0 + q, task.y, task.z, s, L, G, TG, ST, SF, xw);
+						MBIK_PROF_T(c0);
+						if (coop && step) coop_walk<TA, PM>(t, seg, k0 + q, task.y, task.z, s, L, G, TG, ST, SF, xw);
+						MBIK_PROF_T(c1);
+						MBIK_PROF_ADD(19, c0, c1);
 						__syncthreads();
-						V3 tr = v3(0, 0, 0);
-						if (coop && step) tr = coop_sums<TA, PM>(t, seg, task.y, task.z, Gb, TG, s, xw);
-						__syncthreads();
+						MBIK_PROF_T(c2);
+						MBIK_PROF_ADD(21, c1, c2);
 						if (step && task.y == 0)
 							bone_step<false, true, TA, false, false, PM, HOIST, true>(t, seg, k0 + q, 0, 1, coop ? 1 : 0, s, L, G, TG, ST, SF,
-									HS, OE, MS, prev_dev, pre, hoist, nullptr, nullptr, 0, nullptr, xw, tr MBIK_PROF_ARG);
+									HS, OE, MS, prev_dev, pre, hoist, nullptr, nullptr, 0, nullptr, xw MBIK_PROF_ARG);
+						MBIK_PROF_T(c3);
+						MBIK_PROF_ADD(22, c2, c3);
 						__syncthreads();
+						MBIK_PROF_T(c4);
+						MBIK_PROF_ADD(21, c3, c4);
 					}
+					MBIK_PROF_T(cr1);
+					MBIK_PROF_ADD(23, cr0, cr1);
 					r++;
 					continue;
 				}
 			}
+			MBIK_PROF_T(pr0);
 			// rows r .. r1-1: one row, or a packed level (SCHED_CHAIN rows, build_schedule) whose
 			// lanes each run their sequence of segments back to back, without a barrier
 			int r1 = r + 1;
@@ -2161,10 +2139,12 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 				}
 				if (k >= ke) break;
 				bone_step<STAB, HOIST || PL == 2, TA, false, XS, PM, HOIST, false>(t, seg, k, task.y, task.z, task.w & mbik::SCHED_XS, s, L, G, TG,
-						ST, SF, HS, OE, MS, prev_dev, pre, hoist, nullptr, nullptr, 0, nullptr, nullptr, V3{} MBIK_PROF_ARG);
+						ST, SF, HS, OE, MS, prev_dev, pre, hoist, nullptr, nullptr, 0, nullptr, nullptr MBIK_PROF_ARG);
 				k++;
 			}
 			__syncthreads();
+			MBIK_PROF_T(pr1);
+			MBIK_PROF_ADD(18, pr0, pr1);
 			r = r1;
 		}
 	}
@@ -2706,7 +2686,6 @@ int ensure_schedule(mbik_plan *p, int64_t nlaunch) {
 	p->dev.spw = h.spw;
 	p->dev.hs_floats = h.hs_floats;
 	p->dev.rw_xslots = h.rw_xslots;
-	p->dev.rw_xsums = h.rw_xsums;
 	p->dev.n_gck = h.n_gck;
 	p->dev.lds_stride = (mbik::lds_floats_per_skeleton(h) + 3) & ~3;
 	return MBIK_OK;
@@ -2944,8 +2923,8 @@ int launch(mbik_plan *p, int first, int count, const float *pose_in, const float
 	unsigned threads = 64;
 	if (h.wave_roles) {
 		threads = 64u * (unsigned)h.K; // a wave per role
-		// non-finite flags, effector-global exchange, QCP-sum areas
-		lds += 64 * sizeof(int) + (size_t)h.rw_xslots * 12 * 64 * sizeof(float) + (size_t)h.rw_xsums * 11 * 64 * sizeof(double);
+		// non-finite flags; with cooperative rows the targets and the effector-global exchange
+		lds += 64 * sizeof(int) + (h.rw_xslots ? ((size_t)h.P + h.rw_xslots) * 12 * 64 * sizeof(float) : 0);
 		if (lds > 160 * 1024) return fail(MBIK_EUNSUPPORTED, "wave roles: a row's effector-global exchange exceeds the LDS");
 	} else if (helper_on(p)) {
 		static std::once_flag honce;

@@ -2,10 +2,11 @@
 # Diagnostic builds with the product's flags (many_bone_ik_amd/build.py FLAGS) plus one define:
 #   tools/prof_build.sh            -> build/abl/libmbik_abl_PROF.so  (-DMBIK_PROF: per-phase cycle counters)
 #   tools/prof_build.sh REPLAY     -> build/abl/libmbik_replay.so    (-DMBIK_REPLAY: solving wave alone, tools/replay_count.sh)
+# OUT=<path> overrides the output (build/abl/ is not pushed to GPU boxes: .gpurunignore; use build/diag/)
 set -e
 cd "$(dirname "$0")/.."
 mkdir -p build/abl
 FLAGS=$(python3 -c "from many_bone_ik_amd.build import FLAGS; print(' '.join(FLAGS))")
-if [ "$1" = "REPLAY" ]; then DEF=-DMBIK_REPLAY; OUT=build/abl/libmbik_replay.so; else DEF=-DMBIK_PROF; OUT=build/abl/libmbik_abl_PROF.so; fi
+if [ "$1" = "REPLAY" ]; then DEF=-DMBIK_REPLAY; OUT=${OUT:-build/abl/libmbik_replay.so}; else DEF=-DMBIK_PROF; OUT=${OUT:-build/abl/libmbik_abl_PROF.so}; fi
 /opt/rocm/bin/hipcc $FLAGS $DEF many_bone_ik_amd/csrc/solve.hip many_bone_ik_amd/csrc/plan.cpp -o $OUT
 echo $OUT
