@@ -1740,10 +1740,9 @@ __device__ __forceinline__ void global_pass(const DevPlan &t, int seg, const LV 
 }
 
 // Wave roles, cooperative segment (SCHED_XS): wave j of the segment's group of m waves walks the
-// paths of effectors e0+j, e0+j+m, ... from bone-step k's Gb -- the parent's iteration-start
-// global and the bone's local, exactly as bone_step forms them -- with path sharing along its own
-// sequence (the shared depth with a neighbour is the least over the effectors in between, as in
-// the split-exchange branch), and leaves each effector's bone-direction global E in the block's
+// paths of the j-th contiguous run of the segment's effectors from bone-step k's Gb -- the
+// parent's iteration-start global and the bone's local, exactly as bone_step forms them -- with
+// path sharing along the run, and leaves each effector's bone-direction global E in the block's
 // exchange area xw: [slot][12 floats][64 lanes], slot = seg_hbase[seg] + i - e0.
 template <int TA, int PM, class LV, class GV, class FP, class IP>
 __device__ void coop_walk(const DevPlan &t, int seg, int k, int j, int m, size_t s, const LV &L, const GV &G, const FP TG,
@@ -1762,18 +1761,14 @@ __device__ void coop_walk(const DevPlan &t, int seg, int k, int j, int m, size_t
 	const int e0 = t.seg_eff_off[seg], e1 = t.seg_eff_off[seg + 1];
 	const double *hw = t.seg_hw + t.seg_hw_off[seg];
 	float *xe = xw + (size_t)t.seg_hbase[seg] * (12 * 64) + __lane_id();
+	// a contiguous run of the segment's effectors per wave: neighbouring effectors (the fingers of
+	// one arm) share the longest path prefixes, so the run reuses them (PathCk)
+	const int ne = e1 - e0;
+	const int i0 = e0 + (ne * j) / m, i1 = e0 + (ne * (j + 1)) / m;
 	PathCk pc;
 	pc.d = -1;
-	for (int i = e0 + j; i < e1; i += m) {
-		int lc[2] = {0, 0};
-		if (i - m >= e0) {
-			lc[0] = t.seg_eff_lcp[i];
-			for (int u = i - m + 1; u < i; u++) lc[0] = min(lc[0], t.seg_eff_lcp[u]);
-		}
-		if (i + m < e1) {
-			lc[1] = t.seg_eff_lcp[i + 1];
-			for (int u = i + 2; u <= i + m; u++) lc[1] = min(lc[1], t.seg_eff_lcp[u]);
-		}
+	for (int i = i0; i < i1; i++) {
+		const int lc[2] = {i > i0 ? t.seg_eff_lcp[i] : 0, i + 1 < i1 ? t.seg_eff_lcp[i + 1] : 0};
 		X3 E;
 		Headings H; // (unused: the group's first wave builds the headings from E)
 		effector_headings<TA, PM>(t, t.seg_effs[i], d0, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, TG, 0, &pc, lc, &E);
