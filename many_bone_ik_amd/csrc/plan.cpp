@@ -802,9 +802,10 @@ void build_schedule(HostPlan &p, int32_t lanes, int64_t nlaunch, int32_t spw_ove
 	while (best > 1 && resident(best) == 0) best--;
 	int best_c = interval_override > 0 ? interval_override : 1;
 	if (p.wave_roles) {
-		// wave roles: a lane per skeleton, 64 per block of K waves; the state is in device
-		// memory, so LDS holds the topology and the block's 64 non-finite flags only
-		best = 64;
+		// wave roles: a lane per skeleton, 64 per block of K waves (fewer when pinned: partly
+		// filled waves, more blocks for a small launch); the state is in device memory, so LDS
+		// holds the topology, the non-finite flags and the cooperative rows' exchange
+		best = spw_override > 0 ? std::min(64, spw_override) : 64;
 	} else if (spw_override > 0) {
 		best = std::min(spw_override, 64 / K);
 		while (best > 1 && resident(best) == 0) best--;

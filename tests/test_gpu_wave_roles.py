@@ -204,3 +204,18 @@ def test_wave_roles_plan_in_a_group(oracle, mbik, torch_dev):
     assert [p.info()["wave_roles"] for p in plans] == [0, 1, 1]
     for w, o in zip(wls, outs):
         assert_parity(o.cpu().numpy(), oracle.Oracle(w).solve(w.pose, w.targets, threads=8), f"group {w.topo.name}")
+
+
+@pytest.mark.parametrize("cfg,n,k,spw", [(2, 70, 4, 16), (5, 40, 8, 32), (4, 50, 4, 8)])
+def test_wave_roles_partly_filled_waves(oracle, mbik, cfg, n, k, spw):
+    """A pinned skeletons-per-block below 64: each wave's lanes past spw idle at every barrier."""
+    wl = W.generate(cfg, n, first=59000 + cfg)
+    ref = oracle.Oracle(wl).solve(wl.pose, wl.targets, threads=8)
+    plan = Plan.from_workload(wl)
+    plan.set_layout(k, spw, 0)
+    plan.set_waves_per_simd(2)
+    plan.set_wave_roles(1)
+    got = plan.solve_host(wl.pose, wl.targets)
+    info = plan.info()
+    assert info["wave_roles"] == 1 and info["skeletons_per_block"] == spw
+    assert_parity(got, ref, f"C{cfg} wave roles K={k} spw={spw}")
