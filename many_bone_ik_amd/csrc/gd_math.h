@@ -32,7 +32,10 @@ using std::isnan;
 #endif
 enum : unsigned {
 	ABL_SQRT = 1, ABL_ORTHO = 2, ABL_MATMUL = 4, ABL_SOA = 8, ABL_SOALDS = 16, ABL_CONVERT = 32, ABL_SLERP = 64,
-	ABL_SWING = 128, ABL_TWIST = 256, ABL_XCD = 512
+	ABL_SWING = 128, ABL_TWIST = 256, ABL_XCD = 512,
+	// load-site ablations (the same loads, all from one hot address of the skeleton's own state):
+	// the effector path walks' locals, the checkpoint globals, the targets, the other local reads
+	ABL_WALK = 1024, ABL_GCK = 2048, ABL_TGT = 4096, ABL_LOCAL = 8192
 };
 constexpr unsigned kAblate = MBIK_ABLATE;
 

@@ -274,10 +274,17 @@ __device__ __forceinline__ void st_x(BPtr<float> p, const X3 &t) {
 // registers): [r0.x r0.y r1.x r1.y] [r2.x r2.y r0.z r1.z] [o.x o.y o.z r2.z], so every row's and
 // the origin's (x, y) pair lands even-aligned in the loaded registers and needs no moves.
 constexpr int kLocTile = 16;
-template <int BS, int QS, class PT>
+// TAG: 0 the bone locals, 1 the checkpoint globals (timing-only load-site ablations: ABL_LOCAL,
+// ABL_GCK, and ld_walk's ABL_WALK for the effector path walks)
+template <int BS, int QS, class PT, int TAG = 0>
 struct LocV {
 	PT p;
 	__device__ __forceinline__ X3 ld(int i) const {
+		if constexpr ((TAG == 0 && (kAblate & ABL_LOCAL)) || (TAG == 1 && (kAblate & ABL_GCK))) i = 0;
+		return ld_raw(i);
+	}
+	__device__ __forceinline__ X3 ld_walk(int i) const { return ld_raw((kAblate & ABL_WALK) ? 0 : i); }
+	__device__ __forceinline__ X3 ld_raw(int i) const {
 		const auto q = p + BS * i;
 		const float4 a = ld4(q);
 		const float4 b = ld4(q + QS);
@@ -298,11 +305,13 @@ struct LocV {
 };
 using LocContig = LocV<12, 4, float *>;
 // The checkpoint globals G: transform i at p + 12 i (LDS, placements 0 / 1); placement 2 keeps
-// them skeleton-tiled like its locals (LocTiled), so a role's lanes read whole lines.
+// them skeleton-tiled like its locals (GTiled), so a role's lanes read whole lines.
 template <class PT>
-using GFlat = LocV<12, 4, PT>;
+using GFlat = LocV<12, 4, PT, 1>;
 template <class PT>
 using LocTiled = LocV<12 * kLocTile, 4 * kLocTile, PT>;
+template <class PT>
+using GTiled = LocV<12 * kLocTile, 4 * kLocTile, PT, 1>;
 // SoA per-skeleton tables: element (item, field) of skeleton s.
 // (ablation builds only: ABL_SOA reads a hot 16-skeleton working set, ABL_SOALDS skeleton 0's
 // rows copied into LDS)
@@ -535,7 +544,7 @@ template <int TA, int PM = 0, bool DB = true, class FP>
 __device__ __forceinline__ void load_eff(const DevPlan &t, int e, const FP TG, size_t s, const double *hw, EffPre &p) {
 	p.off = t.eff_path_off[e];
 	p.de = t.eff_path_off[e + 1] - p.off - 1;
-	p.T = ld_x(TG + 12 * e);
+	p.T = ld_x(TG + 12 * ((kAblate & ABL_TGT) ? 0 : e));
 	if constexpr (DB) p.Db = ld_soa_basis<TA>(t, t.D, t.eff_bone[e], 9, 0, s);
 	eff_weights<PM>(t, e, hw, p);
 }
@@ -604,24 +613,24 @@ __device__ __forceinline__ void effector_headings(const DevPlan &t, const EffPre
 		// loop's instructions were those moves); the last trip's look-ahead re-reads path[b].
 		auto walk = [&](int a, int b) {
 			if (a > b) return;
-			X3 L0 = L.ld(t.eff_path[off + a]);
+			X3 L0 = L.ld_walk(t.eff_path[off + a]);
 			int d = a;
 			// locals in LDS (placement 0): the first trip peeled out of the loop (C2 -1.1 %; the
 			// device-memory placements keep the plain loop, +0.3 % there;
 			// profiles/r04_walk_peel_ab.jsonl)
 			if constexpr (std::is_same_v<LV, LocContig>) {
 				if (d < b) {
-					const X3 L1 = L.ld(t.eff_path[off + d + 1]);
+					const X3 L1 = L.ld_walk(t.eff_path[off + d + 1]);
 					X = X * L0;
-					L0 = L.ld(t.eff_path[off + min(d + 2, b)]);
+					L0 = L.ld_walk(t.eff_path[off + min(d + 2, b)]);
 					X = X * L1;
 					d += 2;
 				}
 			}
 			for (; d < b; d += 2) {
-				const X3 L1 = L.ld(t.eff_path[off + d + 1]);
+				const X3 L1 = L.ld_walk(t.eff_path[off + d + 1]);
 				X = X * L0;
-				L0 = L.ld(t.eff_path[off + min(d + 2, b)]);
+				L0 = L.ld_walk(t.eff_path[off + min(d + 2, b)]);
 				X = X * L1;
 			}
 			if (d == b) X = X * L0;
@@ -1883,7 +1892,7 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 	using FP = std::conditional_t<PL == 2, BPtr<float>, float *>;
 	using IP = std::conditional_t<PL == 2, BPtr<int>, int *>;
 	using LV = std::conditional_t<PL >= 1, LocTiled<FP>, LocContig>;
-	using GV = std::conditional_t<PL == 2, LocTiled<FP>, GFlat<FP>>;
+	using GV = std::conditional_t<PL == 2, GTiled<FP>, GFlat<FP>>;
 	LV L;
 	GV G;
 	FP S0; // the skeleton's state after its locals (placement 2: and after its checkpoint globals)

@@ -47,9 +47,11 @@ def child(tag: str, cases: str, parity: bool):
         tg = torch.from_numpy(wl.targets).to(dev)
         po_ = torch.empty_like(pi)
         if len(f) >= 8:
-            # pinned layout CFG:N:K:spw:interval:staging:placement:waves[:helper] (bench.py --layout)
+            # pinned layout CFG:N:K:spw:interval:staging:placement:waves[:helper[:roles]] (bench.py --layout)
             k, spw, interval, staging, placement, waves = f[2:8]
             p.set_helper_wave(f[8] if len(f) > 8 else 0)
+            if hasattr(p._L, "mbik_plan_set_wave_roles"):
+                p.set_wave_roles(f[9] if len(f) > 9 else 0)
             p.set_layout(k, spw, interval)
             p.set_heading_staging(staging)
             p.set_locals_placement(placement)
@@ -66,7 +68,7 @@ def child(tag: str, cases: str, parity: bool):
             p.solve(pi.data_ptr(), tg.data_ptr(), po_.data_ptr(), 0, n, st)
         e1.record()
         torch.cuda.synchronize()
-        out[f"c{cfg}_ms"] = round(e0.elapsed_time(e1) / reps, 4)
+        out[f"c{cfg}_ms" if len(f) < 8 else case] = round(e0.elapsed_time(e1) / reps, 4)
         p.close()
     print(json.dumps(out), flush=True)
 
@@ -78,13 +80,14 @@ def main():
     ap.add_argument("--cases", default="2:4096")
     ap.add_argument("--child", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--libdir", default=os.path.join("build", "abl"), help="where the variants' libraries are (build/abl is not pushed to GPU boxes)")
     a = ap.parse_args()
     if a.child:
         return child(a.tags[0], a.cases, not a.no_parity)
     for rep in range(a.reps):
         for tag in a.tags:
             env = dict(os.environ)
-            env["MBIK_LIB_OVERRIDE"] = os.path.join(ROOT, "build", "abl", f"libmbik_abl_{tag}.so")
+            env["MBIK_LIB_OVERRIDE"] = os.path.join(ROOT, a.libdir, f"libmbik_abl_{tag}.so")
             args = [sys.executable, os.path.abspath(__file__), "--child", tag, "--cases", a.cases]
             if a.no_parity or rep > 0:
                 args.append("--no-parity")
