@@ -387,7 +387,15 @@ void mbik_multi_destroy(mbik_multi *multi);
 /* Runs IKBoneSegment3D::segment_solver() once on `segment` (index in post-order segment
  * numbering of mbik_plan_segment_table) for every skeleton in [first, first+count), updating
  * pose_inout in place (device pointers).  No pose write-back conversion is skipped: the
- * output is the Skeleton3D pose of every IK bone after that call. */
+ * output is the Skeleton3D pose of every IK bone after that call.
+ * segment_solver's other arguments are not parameters here:
+ *   p_damp / p_default_damp / p_constraint_mode  come from the plan (mbik_config's bone_damp,
+ *                         default_damp, constraint_mode), as the reference passes its own
+ *                         members (many_bone_ik_3d.cpp:685-693);
+ *   p_current_iteration / p_total_iteration  are accepted by segment_solver but never reach
+ *                         _set_optimal_rotation (ik_bone_segment_3d.cpp:94 calls it without them,
+ *                         so its slerp weight is always 0 and every iteration is alike); the
+ *                         solve has no use for them, and a caller that tracks them loses nothing. */
 int32_t mbik_segment_solve(mbik_plan *plan, int32_t segment, int32_t first, int32_t count, float *pose_inout,
 		const float *targets, void *hip_stream);
 /* Segment table: for each segment, its root bone, tip bone and parent segment (-1). */
