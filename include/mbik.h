@@ -229,8 +229,10 @@ int32_t mbik_plan_set_helper_wave(mbik_plan *plan, int32_t helper);
  * segment with fewer lanes than effectors is solved by one wave, effector by effector, in the
  * reference's order: ik_bone_segment_3d.cpp:210-240).  The whole solve state lives in device
  * memory (state placement 2).  1 on, 0 off, -1 (default) automatic: off until mbik_plan_autotune
- * has timed it.  Plans with stabilization passes, constraint_mode plans and plans whose setup
- * tables need 64-bit indices run without it.  Results do not depend on it. */
+ * has timed it.  constraint_mode plans have their own wave-roles kernel (2, 4 or 8 roles; a
+ * multi-effector segment's effector reads split over its waves where their dirty chains are
+ * disjoint).  Plans with stabilization passes and plans whose setup tables (or constraint_mode
+ * node caches) need 64-bit indices run without it.  Results do not depend on it. */
 int32_t mbik_plan_set_wave_roles(mbik_plan *plan, int32_t roles);
 /* Status of a plan's earlier launches, for callers that poll instead of waiting for the next
  * call's return code (ABI 6): *status = MBIK_STATUS_HELPER_TIMEOUT when a helper-wave launch of

@@ -32,6 +32,11 @@
 // contiguous bytes per load instruction.  With the plain [slot][12][N] rows (round 2) every
 // element was its own dword load and a 16-skeleton group used half of each 128-B line.
 constexpr int kNodeTile = 16;
+#ifndef MBIK_CM_GROUP
+#define MBIK_CM_GROUP 4
+#endif
+constexpr int kChainGroup = MBIK_CM_GROUP; // dirty-chain nodes per load group (CmodeLane::pose_global)
+constexpr unsigned kWaitVmAll = 0x0F70;       // s_waitcnt vmcnt(0) expcnt(7) lgkmcnt(15): gfx9 encoding
 __host__ __device__ __forceinline__ size_t node_at(int slots, size_t s, int k, int f) {
 	return ((s / kNodeTile) * (size_t)slots + (size_t)k) * (12 * kNodeTile) + (size_t)(f >> 2) * (4 * kNodeTile) +
 			(s % kNodeTile) * 4 + (f & 3);
@@ -73,6 +78,7 @@ struct CmodeLane {
 	uint32_t nb;          // NB32: byte offset of this skeleton's slot 0, element 0
 #ifdef MBIK_PROF
 	uint64_t *pf;         // diagnostic counters (tools/prof_cmode.py): see mbik_cmode_kernel
+	int prof_m = 1;       // the running step's lane-group size
 #endif
 
 	__device__ __forceinline__ X3 ld(int k) const {
@@ -148,8 +154,12 @@ struct CmodeLane {
 	// above it is recomputed top-down from its first clean ancestor.
 	// Nodes outside the lane's range are computed but not written; the lowest such node is
 	// recorded in *pend for the after-row cleaning.
-	__device__ X3 pose_global(int b) const {
-		if (!dirty(CK_POSE, b)) return ld(GP(b));
+	// dq (bdir_global): also loads bone b's bone-direction basis D, with the chain's last group.
+	__device__ __forceinline__ X3 pose_global(int b, B3 *dq = nullptr) const {
+		if (!dirty(CK_POSE, b)) {
+			if (dq) *dq = ld_soa_basis<NB32 ? kTab32 : kTab64>(t, t.D, b, 9, 0, s);
+			return ld(GP(b));
+		}
 		MBIK_PROF_T(q0);
 		int n = 0, x = b, pp;
 		for (;;) {
@@ -158,28 +168,41 @@ struct CmodeLane {
 			if (pp < 0 || !dirty(CK_POSE, pp)) break;
 			x = pp;
 		}
-		// Top-down over stk[n-1] (= x) .. stk[0] (= b).  The chain's locals are known now, so
-		// their loads run two nodes ahead of the products: a chain of n dependent node-cache
-		// misses becomes ~n/3 round trips (the products and their order are unchanged; three
-		// ahead measured 0.5 % slower on C5).
-		const X3 Lx = ld(LP(x));
-		X3 La = n >= 2 ? ld(LP(stk[64 * (n - 2)])) : Lx;
-		X3 Lb = n >= 3 ? ld(LP(stk[64 * (n - 3)])) : Lx;
-		X3 G = pp >= 0 ? ld(GP(pp)) * Lx : (pp == mbik::POSE_PARENT_ORIGIN ? xid() * Lx : Lx);
-		keep(x, G);
-		for (int i = n - 2; i >= 0; i--) {
-			const X3 Lc = La;
-			La = Lb;
-			if (i >= 2) Lb = ld(LP(stk[64 * (i - 2)]));
-			x = stk[64 * i];
-			G = G * Lc;
-			keep(x, G);
+		// Top-down over stk[n-1] (= x) .. stk[0] (= b), kChainGroup nodes at a time: a group's
+		// locals (and, first, the clean parent's global) are loaded together, then its products
+		// run and its globals are stored.  gfx9's vmcnt counts stores as well as loads, and with
+		// both pending a wait can only be for all of them: a load issued after a store waits for
+		// that store's write to complete (~3,000 cycles on a busy chip).  Grouped, a chain pays
+		// that round trip once per group instead of once per node.  The products and their order
+		// are unchanged.
+		X3 G;
+		for (int i = n - 1; i >= 0; i -= kChainGroup) {
+			X3 Lq[kChainGroup];
+#pragma unroll
+			for (int u = 0; u < kChainGroup; u++)
+				if (i - u >= 0) Lq[u] = ld(LP(stk[64 * (i - u)]));
+			X3 Gp;
+			if (i == n - 1 && pp >= 0) Gp = ld(GP(pp));
+			if (dq && i < kChainGroup) *dq = ld_soa_basis<NB32 ? kTab32 : kTab64>(t, t.D, b, 9, 0, s);
+			// every load of the group lands before the group's first store (else the compiler's
+			// wait for a later local, now behind a store, would be for that store too)
+			__builtin_amdgcn_s_waitcnt(kWaitVmAll);
+#pragma unroll
+			for (int u = 0; u < kChainGroup; u++) {
+				if (i - u < 0) break;
+				if (u == 0 && i == n - 1)
+					G = pp >= 0 ? Gp * Lq[0] : (pp == mbik::POSE_PARENT_ORIGIN ? xid() * Lq[0] : Lq[0]);
+				else
+					G = G * Lq[u];
+				keep(stk[64 * (i - u)], G);
+			}
 		}
 #ifdef MBIK_PROF
 		MBIK_PROF_T(q1);
 		pf[4] += q1 - q0;
 		pf[5] += n;
 		pf[6] += 1;
+		if (prof_m > 1) pf[11] += n;
 #endif
 		return G;
 	}
@@ -189,15 +212,20 @@ struct CmodeLane {
 			set_clean(CK_POSE, x);
 		} else {
 			*pend = x; // visited top-down: ends as the lowest outside node (the segment root's parent)
+#ifdef MBIK_PROF
+			pf[10] += 1;
+#endif
 		}
 	}
 	// IKBone3D::get_bone_direction_global_pose (ik_bone_3d.cpp:157-159): local = (D, 0).
-	__device__ X3 bdir_global(int b) const {
+	__device__ __forceinline__ X3 bdir_global(int b) const {
 		if (!dirty(CK_BDIR, b)) return ld(GD(b));
 #ifdef MBIK_PROF
 		pf[9] += 1;
 #endif
-		const X3 G = pose_global(b) * X3{ld_soa_basis<NB32 ? kTab32 : kTab64>(t, t.D, b, 9, 0, s), v3(0, 0, 0)};
+		B3 D;
+		const X3 Gp = pose_global(b, &D);
+		const X3 G = Gp * X3{D, v3(0, 0, 0)};
 		st(GD(b), G);
 		set_clean(CK_BDIR, b);
 		return G;
@@ -205,12 +233,12 @@ struct CmodeLane {
 	// A read whose value is not used (the heading builds' reads in a plain constraint_mode
 	// step only matter for the caches they refresh): the recomputation of a dirty node, no
 	// load of a clean one.
-	__device__ void bdir_touch(int b) const {
+	__device__ __forceinline__ void bdir_touch(int b) const {
 		if (dirty(CK_BDIR, b)) (void)bdir_global(b);
 	}
 	// constraint_orientation_transform: parent = the parent bone's pose node; its local stays
 	// the identity (only set_global_pose copies an origin into it, ik_bone_3d.cpp:145-151).
-	__device__ X3 orient_global(int b) const {
+	__device__ __forceinline__ X3 orient_global(int b) const {
 		const int k = GC(t.bone_cons[b]);
 		if (!dirty(CK_COR, b)) return ld(k);
 		const X3 G = pose_global(t.bone_pose_parent[b]) * xid();
@@ -219,7 +247,7 @@ struct CmodeLane {
 		return G;
 	}
 	// constraint_twist_transform: local = (twist frame basis, 0) (ik_kusudama_3d.cpp:37-89).
-	__device__ X3 twist_global(int b) const {
+	__device__ __forceinline__ X3 twist_global(int b) const {
 		const int slot_ = t.bone_cons[b];
 		const int k = GT(slot_);
 		if (!dirty(CK_CTW, b)) return ld(k);
@@ -244,8 +272,11 @@ struct CmodeLane {
 // the same cached bits and dirty words as the reference's sequential loop; lanes that share a
 // chain recompute it alike.  Stabilized segments keep every read on every lane: the MSD loop
 // needs each effector's target-heading origin on the lane that sums them.
+// reads false (wave roles, SCHED_CMSPLIT): the effector reads were made by the segment's waves
+// before (cmode_coop_step); the step starts at the solved bone's own read.
 template <bool STAB, bool NB32>
-__device__ void cmode_step(const CmodeLane<NB32> &C, int seg, int k, int j, int m, const float *tg, float *OE, double &prev_dev) {
+__device__ __forceinline__ void cmode_step(const CmodeLane<NB32> &C, int seg, int k, int j, int m, const float *tg, float *OE, double &prev_dev,
+		bool reads = true) {
 	const int ls = 64;
 	const DevPlan &t = C.t;
 	const int b = t.seg_bones[k];
@@ -254,10 +285,11 @@ __device__ void cmode_step(const CmodeLane<NB32> &C, int seg, int k, int j, int 
 	const int flags = t.bone_flags[b];
 #ifdef MBIK_PROF
 	uint64_t *pf = C.pf;
+	const_cast<CmodeLane<NB32> &>(C).prof_m = m;
 #endif
 	MBIK_PROF_T(c0);
 	const int i0 = stab ? e0 : e0 + j, di = stab ? 1 : m;
-	for (int i = i0; i < e1; i += di) {
+	for (int i = reads ? i0 : e1; i < e1; i += di) {
 		const int e = t.seg_effs[i];
 		if (stab) {
 			const X3 E = C.bdir_global(t.eff_bone[e]);
@@ -324,6 +356,10 @@ __device__ void cmode_step(const CmodeLane<NB32> &C, int seg, int k, int j, int 
 		}
 		MBIK_PROF_T(c3);
 		MBIK_PROF_ADD(2, c2, c3);
+#ifdef MBIK_PROF
+		if (m > 1) pf[12] += c3 - c0;
+		if (e1 - e0 > 1) pf[13] += c3 - c0;
+#endif
 		if (!stab) break;
 		// _get_manual_msd(tip_headings_uniform, target_headings, weights) (:114-127)
 		const double *hw = t.seg_hw + t.seg_hw_off[seg];
@@ -414,7 +450,9 @@ __global__ __launch_bounds__(64 * kCmodeMaxWaves) void mbik_cmode_kernel(DevPlan
 			&pend, buf_rsrc(c.node, node_bytes), (uint32_t)(n0 * 4)};
 #ifdef MBIK_PROF
 	// 0 effector heading reads, 1 swing, 2 twist, 4 dirty pose chains (cycles), 5 chain nodes,
-	// 6 dirty pose reads, 7 total, 8 after-row cleaning, 9 bone-direction recomputes
+	// 6 dirty pose reads, 7 total, 8 after-row cleaning, 9 bone-direction recomputes, 10 chain
+	// nodes above the segment root (private), 11 chain nodes in lane groups of m > 1, 12 / 13
+	// step cycles with m > 1 / in multi-effector segments
 	uint64_t pfa[24] = {};
 	C.pf = pfa;
 	uint64_t *pf = pfa;
@@ -548,6 +586,196 @@ __global__ __launch_bounds__(64 * kCmodeMaxWaves) void mbik_cmode_kernel(DevPlan
 	}
 	write_nonfinite(t, valid, bad, g, role, local);
 	__syncthreads();
+	if (valid)
+		for (int w = role; w < 4 * c.W; w += K) c.dirty[(size_t)w * t.N + s] = C.dl[spw * w];
+#ifdef MBIK_PROF
+	MBIK_PROF_T(k1);
+	pfa[7] += k1 - k0;
+	if (valid)
+		for (int i = 0; i < 24; i++) atomicAdd(&g_mbik_prof[i], (unsigned long long)pfa[i]);
+#endif
+}
+
+// constraint_mode with wave roles (HostPlan::cm_roles; mbik_plan_set_wave_roles): a block is KW
+// waves x c.spw skeletons, a lane per skeleton and a wave per role of the sibling schedule.  A
+// wave then follows one segment for all its skeletons -- its topology is wave-uniform and its
+// dirty chains have the same shape on every lane -- and each role waits for its own node-cache
+// misses instead of for the union of the wave's roles' paths.  LDS: the topology and pre-order
+// tables, the block's dirty words (shared by a skeleton's waves through LDS atomics, as the
+// classic kernel shares them between lanes), per wave its lanes' chain stacks, then the row's
+// pending cleanings ([KW][4][64]) and the non-finite flags (64).  No stabilization.
+//
+// Rows with a SCHED_CMSPLIT segment (SCHED_COOP): each bone-step is three phases between two
+// block barriers -- the group's first wave reads the first effector (the reference's first
+// read, which cleans the chain every later read of the step starts from), then every wave of
+// the group reads its clusters of the other effectors (plan.cpp cm_split_groups: effectors
+// whose dirty chains overlap beyond the first one's path stay on one wave, in order), then the
+// first wave runs the rest of the step (the bone's own read, the swing and the twist).  The other
+// tasks of such a row run their whole step in the last phase.  Sibling segments touch disjoint
+// subtrees, and the first wave's writes reach the other waves through the barriers.
+template <bool NB32, bool CHAIN, int KW>
+__global__ __launch_bounds__(64 * KW) void mbik_cmode_kernel_rw(DevPlan t, CmodeState c, int first, int count,
+		const float *__restrict__ pose_in, const float *__restrict__ targets, float *__restrict__ pose_out, int iterations,
+		int seg_lo, int seg_hi) {
+	extern __shared__ float4 lds4[];
+	const int lane = threadIdx.x & 63;
+	const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+	{
+		uint4 *dst = reinterpret_cast<uint4 *>(lds4);
+		for (int i = threadIdx.x; i < (t.topo_words >> 2); i += 64 * KW) dst[i] = t.topo_blob[i];
+	}
+	const uint32_t *topo = reinterpret_cast<const uint32_t *>(lds4);
+#define MBIK_REPOINT(T, name) t.name = reinterpret_cast<const T *>(topo + t.o_##name);
+	MBIK_TOPO_TABLES(MBIK_REPOINT)
+#undef MBIK_REPOINT
+	const int B = t.B, K = KW;
+	const int spw = c.spw; // skeletons of this block (<= 64)
+	int *pre = reinterpret_cast<int *>(lds4) + t.topo_words;
+	int *sub = pre + B;
+	for (int i = threadIdx.x; i < B; i += 64 * KW) {
+		pre[i] = c.pre[i];
+		sub[i] = c.sub[i];
+	}
+	uint32_t *dl0 = reinterpret_cast<uint32_t *>(sub + B);                        // [4 W][spw]
+	int *stks = reinterpret_cast<int *>(dl0 + (size_t)4 * c.W * spw);           // [KW][maxd][64]
+	int *pv = stks + (size_t)KW * c.maxd * 64;                                   // [KW][4][64]
+	int *nf = pv + KW * 4 * 64;                                                   // [64]
+	const int g = lane, role = wv;
+	const int local = xcd_block() * spw + g;
+	const bool valid = g < spw && local < count;
+	const size_t s = (size_t)first + (valid ? local : 0);
+	int pend = -1;
+	const int slots = 3 * B + 2 * t.NC;
+	const uint32_t node_bytes = NB32 ? (uint32_t)(node_area_floats(slots, (size_t)t.N) * 4) : 0u;
+	const size_t n0 = node_at(slots, s, 0, 0);
+	CmodeLane<NB32> C{t, c, s, c.node + n0, slots, dl0 + (g < spw ? g : 0), spw, stks + (size_t)wv * c.maxd * 64 + lane, pre, sub, 0,
+			0x7fffffff, &pend, buf_rsrc(c.node, node_bytes), (uint32_t)(n0 * 4)};
+#ifdef MBIK_PROF
+	uint64_t pfa[24] = {};
+	C.pf = pfa;
+	uint64_t *pf = pfa;
+#endif
+	MBIK_PROF_T(k0);
+	if (wv == 0) nf[lane] = 0;
+	if (valid)
+		for (int w = role; w < 4 * c.W; w += K) C.dl[spw * w] = c.dirty[(size_t)w * t.N + s];
+	__syncthreads();
+	// _update_ik_bones_transform (:91-102): set_transform of every list bone's pose
+	if (valid)
+		for (int b = role; b < B; b += K) {
+			if (!(t.bone_flags[b] & mbik::BF_IN_LIST)) continue;
+			const X3 L = pose_to_xform(pose_in + ((size_t)local * B + b) * 10);
+			if (!eq(C.ld(C.LP(b)), L)) {
+				C.st(C.LP(b), L);
+				C.propagate(b);
+			}
+		}
+	__syncthreads();
+	const float *tg = targets + (size_t)local * t.P * 12;
+	double prev_dev = INFINITY; // (stabilization only)
+	auto set_range = [&](int seg) {
+		const int root = t.seg_bones[t.seg_bone_off[seg + 1] - 1];
+		C.lo = pre[root];
+		C.hi = pre[root] + sub[root];
+	};
+	for (int it = 0; it < iterations; it++) {
+		for (int r = 0; r < t.nrows;) {
+			const int4 task0 = t.sched[r * K + role];
+			int r1 = r + 1;
+			if constexpr (CHAIN)
+				while (r1 < t.nrows && (t.sched[r1 * K].w & mbik::SCHED_CHAIN)) r1++;
+			int p1 = -1, p2 = -1, p3 = -1;
+			if (task0.w & mbik::SCHED_COOP) {
+				// (a cooperative row is one row: packed levels have one-wave tasks only)
+				const int seg = task0.x, j = task0.y, m = task0.z;
+				const bool act = valid && seg >= 0 && seg >= seg_lo && seg <= seg_hi;
+				const bool split = (task0.w & mbik::SCHED_CMSPLIT) != 0;
+				const int nq = row_steps(t, r, seg_lo, seg_hi);
+				int k0 = 0, ns = 0, e0 = 0, e1 = 0;
+				if (seg >= 0) {
+					set_range(seg);
+					k0 = t.seg_bone_off[seg];
+					ns = t.seg_bone_off[seg + 1] - k0;
+					e0 = t.seg_eff_off[seg];
+					e1 = t.seg_eff_off[seg + 1];
+				}
+				for (int q = 0; q < nq; q++) {
+					const bool step = act && q < ns;
+					if (split && step && j == 0) C.bdir_touch(t.eff_bone[t.seg_effs[e0]]);
+					__syncthreads();
+					if (split && step)
+						for (int i = e0 + 1; i < e1; i++)
+							if (t.seg_eff_grp[i] == j) C.bdir_touch(t.eff_bone[t.seg_effs[i]]);
+					__syncthreads();
+					if (step && j == 0) cmode_step<false, NB32>(C, seg, k0 + q, 0, 1, tg, nullptr, prev_dev, !split);
+				}
+			} else {
+				// rows r .. r1-1: one row, or a packed level run back to back by each wave (the
+				// classic kernel's CHAIN loop); a group of several waves without a split runs on
+				// its first wave
+				int rr = r - 1, k = 0, ke = 0, seg = 0;
+				for (;;) {
+					while (k >= ke && rr + 1 < r1) {
+						const int4 task = t.sched[++rr * K + role];
+						if (valid && task.x >= 0 && task.x >= seg_lo && task.x <= seg_hi && task.y == 0) {
+							if (pend >= 0) {
+								p3 = p2;
+								p2 = p1;
+								p1 = pend;
+								pend = -1;
+							}
+							seg = task.x;
+							set_range(seg);
+							k = t.seg_bone_off[seg];
+							ke = t.seg_bone_off[seg + 1];
+						}
+					}
+					if (k >= ke) break;
+					cmode_step<false, NB32>(C, seg, k, 0, 1, tg, nullptr, prev_dev);
+					k++;
+				}
+			}
+			// The cleaning the reference's first read above a segment root did, for every pending
+			// chain of the row (siblings share them; a chain is computed once and then clean): the
+			// first wave cleans them all, lane by lane for its own skeleton.
+			pv[(role * 4 + 0) * 64 + lane] = pend;
+			pv[(role * 4 + 1) * 64 + lane] = p1;
+			pv[(role * 4 + 2) * 64 + lane] = p2;
+			pv[(role * 4 + 3) * 64 + lane] = p3;
+			pend = -1;
+			__syncthreads();
+			MBIK_PROF_T(rc0);
+			if (wv == 0 && valid) {
+				C.lo = 0;
+				C.hi = 0x7fffffff;
+				for (int w = 0; w < K; w++)
+					for (int q = 0; q < 4; q++) {
+						const int x = pv[(w * 4 + q) * 64 + lane];
+						if (x >= 0) (void)C.pose_global(x);
+					}
+			}
+			MBIK_PROF_T(rc1);
+			MBIK_PROF_ADD(8, rc0, rc1);
+			__syncthreads();
+			r = r1;
+		}
+	}
+	bool bad = false;
+	if (valid) {
+		for (int b = role; b < B; b += K) {
+			float *dst = pose_out + ((size_t)local * B + b) * 10;
+			if (t.bone_flags[b] & mbik::BF_IN_LIST) {
+				bad |= write_pose(C.ld(C.LP(b)), dst);
+			} else {
+				const float *src = pose_in + ((size_t)local * B + b) * 10;
+				for (int f = 0; f < 10; f++) dst[f] = src[f];
+			}
+		}
+	}
+	// a skeleton's bones are written by all its waves: their flags meet in LDS
+	if (valid && bad) nf[lane] = 1;
+	__syncthreads();
+	if (t.nonfinite && valid && wv == 0) t.nonfinite[local] = nf[lane] != 0;
 	if (valid)
 		for (int w = role; w < 4 * c.W; w += K) c.dirty[(size_t)w * t.N + s] = C.dl[spw * w];
 #ifdef MBIK_PROF

@@ -574,6 +574,7 @@ int64_t topology_bytes(const HostPlan &p) {
 	ints(p.cons_ncones.size()); ints(2 * p.seg_hw.size()); ints(2 * p.seg_cos_half_damp.size());
 	ints(4 * p.seg_bones.size() + 3); // step_rec, 16-byte aligned
 	ints(p.seg_effs.size() + 1);      // seg_eff_lcp
+	ints(p.seg_effs.size() + 1);      // seg_eff_grp
 	return (w + 4) * 4;
 }
 
@@ -583,9 +584,65 @@ static int ceil_log2(int v) {
 	return l;
 }
 
+// constraint_mode, wave roles: the split of a multi-effector segment's effector reads over its
+// group of m waves.  The reference reads the effectors in order, each read cleaning the dirty
+// chain above its effector.  After the first effector's read (alone), effectors a and b may be
+// read concurrently on separate waves only if every node they share -- the prefix of depth
+// lcp(a, b) of both paths from the root -- lies on the first effector's path, which that read
+// has cleaned: lcp(a, b) <= min(lcp(0, a), lcp(0, b)).  Effectors that fail this (transitively)
+// form a cluster that one wave reads in the reference's order; clusters go to waves longest
+// first.  A recomputed node's value does not depend on which read recomputes it (nothing above
+// the reads changes during them), so the caches end as after the sequential reads.
+// Writes seg_eff_grp for the segment; false when fewer than two clusters (no split).
+static bool cm_split_groups(HostPlan &p, int sg, int m) {
+	const int e0 = p.seg_eff_off[sg], e1 = p.seg_eff_off[sg + 1], n = e1 - e0;
+	auto plen = [&](int a) { const int e = p.seg_effs[a]; return p.eff_path_off[e + 1] - p.eff_path_off[e]; };
+	auto lcp = [&](int a, int b) {
+		const int ea = p.seg_effs[a], eb = p.seg_effs[b];
+		const int la = plen(a), lb = plen(b);
+		int l = 0;
+		while (l < la && l < lb && p.eff_path[p.eff_path_off[ea] + l] == p.eff_path[p.eff_path_off[eb] + l]) l++;
+		return l;
+	};
+	if (n > 256) return false; // (the pairwise test is quadratic; such segments run on one wave)
+	std::vector<int> l0(n, 0);
+	for (int a = 1; a < n; a++) l0[a] = lcp(e0, e0 + a);
+	std::vector<int> par(n); // clusters of effectors e0 + 1 .. : union over the pairs that fail the test
+	for (int i = 0; i < n; i++) par[i] = i;
+	auto find = [&](int x) {
+		while (par[x] != x) x = par[x] = par[par[x]];
+		return x;
+	};
+	for (int a = 1; a < n; a++)
+		for (int b = a + 1; b < n; b++)
+			if (lcp(e0 + a, e0 + b) > std::min(l0[a], l0[b])) par[find(b)] = find(a);
+	std::vector<int> roots;
+	std::vector<int64_t> cost(n, 0);
+	for (int a = 1; a < n; a++) {
+		const int r = find(a);
+		if (cost[r] == 0) roots.push_back(r);
+		cost[r] += std::max(1, plen(e0 + a) - l0[a]); // the nodes below the first path
+	}
+	if ((int)roots.size() < 2) return false;
+	std::stable_sort(roots.begin(), roots.end(), [&](int x, int y) { return cost[x] > cost[y]; });
+	std::vector<int64_t> load(m, 0);
+	std::vector<int> wave(n, 0);
+	for (int r : roots) {
+		int w = 0;
+		for (int q = 1; q < m; q++)
+			if (load[q] < load[w]) w = q;
+		wave[r] = w;
+		load[w] += cost[r];
+	}
+	for (int a = 1; a < n; a++) p.seg_eff_grp[e0 + a] = wave[find(a)];
+	p.seg_eff_grp[e0] = 0;
+	return true;
+}
+
 void build_schedule(HostPlan &p, int32_t lanes, int64_t nlaunch, int32_t spw_override, int32_t interval_override,
 		BlocksPerCU blocks_per_cu, void *ctx, int cus) {
 	p.seg_eff_lcp.assign(p.seg_effs.size() + 1, 0);
+	p.seg_eff_grp.assign(p.seg_effs.size() + 1, 0);
 	for (int sg = 0; sg < p.NS; sg++)
 		for (int i = p.seg_eff_off[sg] + 1; i < p.seg_eff_off[sg + 1]; i++) {
 			const int a = p.seg_effs[i - 1], b = p.seg_effs[i];
@@ -668,6 +725,7 @@ void build_schedule(HostPlan &p, int32_t lanes, int64_t nlaunch, int32_t spw_ove
 		for (size_t start = 0; start < l.size(); start += K) {
 			int cnt = (int)std::min<size_t>(K, l.size() - start);
 			int m = K >> ceil_log2(cnt);
+			bool cmsplit_row = false;
 			if (p.wave_roles) {
 				// Wave roles: each segment of the row on a group of m waves.  A segment of two or
 				// more effectors is solved cooperatively (SCHED_XS): its waves split the effector path
@@ -704,10 +762,17 @@ void build_schedule(HostPlan &p, int32_t lanes, int64_t nlaunch, int32_t spw_ove
 				// over the group's lanes and exchange the headings lane to lane
 				// (the two-waves-per-SIMD build is the one that serves them; one wave: solo)
 				const bool xs = solo && multi && m >= 2 && (p.staging == 4 || p.staging == 5) && p.waves_per_simd == 2;
+				// constraint_mode with wave roles: the group's waves split the step's effector reads when
+				// into two or more clusters (cm_split_groups); else the group's first wave runs the segment alone
+				const bool cms = p.constraint_mode && p.cm_roles && multi && m >= 2 && cm_split_groups(p, sg, m);
+				cmsplit_row |= cms;
 				for (int j = 0; j < m; j++)
-					row[i * m + j] = xs ? SchedTask{sg, j, m, SCHED_XS} : (solo ? SchedTask{sg, 0, 1, 0} : SchedTask{sg, j, m, 0});
+					row[i * m + j] = xs ? SchedTask{sg, j, m, SCHED_XS}
+										: (solo ? SchedTask{sg, 0, 1, 0} : SchedTask{sg, j, m, cms ? SCHED_CMSPLIT : 0});
 				p.has_xs |= xs;
 			}
+			if (cmsplit_row)
+				for (auto &tk : row) tk.flags |= SCHED_COOP;
 			p.sched.insert(p.sched.end(), row.begin(), row.end());
 			p.nrows++;
 		}

@@ -66,7 +66,11 @@ struct SchedTask {
 // solved by a group of waves (SCHED_XS, m > 1): the group's waves walk alternate effectors' paths
 // and leave the effector globals in LDS, the group's first wave consumes them all in order and runs
 // the step's rotation chain; the whole block meets at two barriers per bone-step of the row.
-constexpr int32_t SCHED_XS = 1, SCHED_CHAIN = 2, SCHED_COOP = 4;
+// SCHED_CMSPLIT (constraint_mode with wave roles): a multi-effector segment whose group of m waves
+// splits the step's effector reads -- the first effector's read alone, then the others, whose
+// dirty chains are disjoint once it has cleaned its own, over the group's waves (cmode.h); its
+// row's tasks carry SCHED_COOP too (two block barriers per bone-step).
+constexpr int32_t SCHED_XS = 1, SCHED_CHAIN = 2, SCHED_COOP = 4, SCHED_CMSPLIT = 8;
 
 struct HostPlan {
 	// ---- topology (shared by the batch) ----
@@ -135,6 +139,9 @@ struct HostPlan {
 	// wave roles: effector-global exchange slots of the cooperative rows (SCHED_COOP), the most any
 	// row needs; a slot is 12 floats x 64 lanes of LDS.  seg_hbase[seg] is the segment's first slot.
 	int32_t rw_xslots = 0;
+	// constraint_mode with wave roles (cmode.h): the K roles are the block's waves, a lane per
+	// skeleton; build_schedule marks the splittable multi-effector tasks (SCHED_CMSPLIT).
+	int32_t cm_roles = 0;
 	// Iteration-start globals kept in LDS only for checkpoint bones: every g_interval-th bone
 	// of a segment counted from its root (the root included) and every parent of a segment
 	// root; a bone-step rebuilds its parent's global from the nearest checkpoint above it.
@@ -150,6 +157,10 @@ struct HostPlan {
 	// shares with the previous effector's of the same segment (0 for a segment's first), plus
 	// a trailing 0.  The solve reuses the previous effector's walk down to that depth.
 	std::vector<int32_t> seg_eff_lcp;
+	// constraint_mode with wave roles, per seg_effs index i of a SCHED_CMSPLIT segment: the wave of
+	// the segment's group that reads effector i after the first effector's read (cm_split_groups);
+	// 0 elsewhere, plus a trailing 0.
+	std::vector<int32_t> seg_eff_grp;
 	std::vector<SchedTask> sched;                   // [nrows][K]
 	int32_t nrows = 0;
 	// ---- per skeleton, SoA [item][field][N] ----

@@ -34,6 +34,7 @@
 #include <mutex>
 #include <string>
 #include <vector>
+#include <array>
 
 #include "gd_math.h"
 #include "plan.h"
@@ -72,7 +73,7 @@ namespace {
 	X(int, seg_eff_off) X(int, seg_effs) X(int, seg_eff_hoff) X(int, seg_nh) X(int, seg_flags)         \
 	X(int, seg_hw_off) X(int, eff_bone) X(int, eff_path_off) X(int, eff_path) X(float, eff_prio)       \
 	X(int, cons_ncones) X(float, seg_wsum2) X(int, seg_hbase) X(int, bone_gslot) X(double, seg_hw) X(double, seg_cos_half_damp) X(int4, sched) \
-	X(int4, step_rec) X(int, seg_eff_lcp)
+	X(int4, step_rec) X(int, seg_eff_lcp) X(int, seg_eff_grp)
 
 struct DevPlan {
 	int B, P, NS, NC, max_cones, nrows, K, log2K, spw, lds_stride;
@@ -2615,6 +2616,18 @@ int ensure_schedule(mbik_plan *p, int64_t nlaunch) {
 			h.wave_roles = 0;
 		}
 	}
+	// constraint_mode with wave roles (cmode.h mbik_cmode_kernel_rw): K = 2, 4 or 8 waves per block
+	h.cm_roles = 0;
+	if (h.constraint_mode && p->roles_override == 1 && h.stabilization_passes == 0 && tables_fit_32(p) &&
+			node_area_floats(3 * h.B + 2 * h.NC, (size_t)h.N) * sizeof(float) < (size_t(1) << 32)) {
+		int roles = 1;
+		while (roles < (lanes > 0 ? lanes : kCmodeLanes)) roles <<= 1;
+		roles = std::min(8, roles);
+		if (roles >= 2) {
+			lanes = roles;
+			h.cm_roles = 1;
+		}
+	}
 	if (h.state_hbm >= 1 && !tables_fit_32(p))
 		return fail(MBIK_EUNSUPPORTED, "state placements 1 and 2 need every setup table < 4 GiB (fewer skeletons per plan)");
 	if (h.state_hbm >= 1 && !p->d_locals) {
@@ -2630,7 +2643,7 @@ int ensure_schedule(mbik_plan *p, int64_t nlaunch) {
 	// two-wave build solves those segments alone (4 -> 0) or staged (5 -> 2)
 	if (h.waves_per_simd == 2 && !tables_fit_32(p) && h.staging >= 4) h.staging = h.staging == 4 ? 0 : 2;
 	mbik::build_schedule(h, lanes, nlaunch, p->spw_override, p->interval_override, blocks_per_cu, p, p->cu_count);
-	if (lanes == 0 && h.constraint_mode && h.K > kCmodeLanes)
+	if (lanes == 0 && h.constraint_mode && h.K > kCmodeLanes && !h.cm_roles)
 		mbik::build_schedule(h, kCmodeLanes, nlaunch, p->spw_override, p->interval_override, blocks_per_cu, p, p->cu_count);
 	if (h.state_hbm == 2) {
 		// the whole state in device memory: one skeleton's LDS layout per skeleton (the locals
@@ -2673,7 +2686,7 @@ int ensure_schedule(mbik_plan *p, int64_t nlaunch) {
 		p->dev.state_stride = stride;
 	}
 	if (p->sched_K == h.K && p->sched_c == h.g_interval && p->sched_staging == h.staging &&
-			p->sched_locals == h.state_hbm && p->sched_roles == h.wave_roles && p->d_sched) {
+			p->sched_locals == h.state_hbm && p->sched_roles == (h.wave_roles | h.cm_roles << 1) && p->d_sched) {
 		p->dev.spw = h.spw;
 		return MBIK_OK;
 	}
@@ -2683,7 +2696,7 @@ int ensure_schedule(mbik_plan *p, int64_t nlaunch) {
 	p->sched_c = h.g_interval;
 	p->sched_staging = h.staging;
 	p->sched_locals = h.state_hbm;
-	p->sched_roles = h.wave_roles;
+	p->sched_roles = h.wave_roles | h.cm_roles << 1;
 	p->dev.nrows = h.nrows;
 	p->dev.K = h.K;
 	p->dev.log2K = h.log2K;
@@ -2712,6 +2725,8 @@ struct CmShape {
 };
 CmShape cmode_shape_of(const mbik_plan *p, int64_t count) {
 	const mbik::HostPlan &h = p->host;
+	if (h.cm_roles) // wave roles: a block is K waves x spw skeletons (64, halved cm_spw_div times)
+		return CmShape{p->spw_override > 0 ? std::min(64, p->spw_override) : std::max(1, 64 >> std::max(0, p->cm_spw_div)), 1};
 	const int full = 64 >> h.log2K;
 	const int spw = p->spw_override > 0 ? std::min(full, p->spw_override) : std::max(1, full >> std::max(0, p->cm_spw_div));
 	int wpb = kCmodeMaxWaves;
@@ -2723,6 +2738,10 @@ CmShape cmode_shape_of(const mbik_plan *p, int64_t count) {
 }
 size_t cmode_lds_bytes(const mbik_plan *p, CmShape sh) {
 	const mbik::HostPlan &h = p->host;
+	if (h.cm_roles) // topology, pre-order tables, dirty words, per wave the chain stacks, pending cleanings, flags
+		return ((size_t)p->dev.topo_words + 2 * (size_t)h.B + (size_t)sh.spw * 4 * p->cm.W + (size_t)h.K * 64 * p->cm.maxd +
+					   (size_t)h.K * 4 * 64 + 64) *
+				sizeof(float);
 	return ((size_t)p->dev.topo_words + 2 * (size_t)h.B + (size_t)sh.wpb * cmode_wave_words(p, sh.spw)) * sizeof(float);
 }
 void cmode_shape(mbik_plan *p, int count) {
@@ -2913,7 +2932,22 @@ int launch(mbik_plan *p, int first, int count, const float *pose_in, const float
 							  : (h.stabilization_passes > 0 ? (nb32 ? mbik_cmode_kernel<true, true> : mbik_cmode_kernel<true, false>)
 												 : (nb32 ? mbik_cmode_kernel<false, true> : mbik_cmode_kernel<false, false>));
 		const int per_block = p->cm.spw * p->cm.wpb;
-		hipLaunchKernelGGL(ck, dim3((unsigned)((count + per_block - 1) / per_block)), dim3(64 * p->cm.wpb), clds, stream, p->dev,
+		unsigned threads = 64 * p->cm.wpb;
+		if (h.cm_roles) {
+			// wave roles: K waves x spw skeletons per block (ensure_schedule: K in {2, 4, 8}, 32-bit addressing)
+			using CK = decltype(ck);
+			static const CK krw[2][3] = {{mbik_cmode_kernel_rw<true, false, 2>, mbik_cmode_kernel_rw<true, false, 4>, mbik_cmode_kernel_rw<true, false, 8>},
+					{mbik_cmode_kernel_rw<true, true, 2>, mbik_cmode_kernel_rw<true, true, 4>, mbik_cmode_kernel_rw<true, true, 8>}};
+			static std::once_flag ronce;
+			std::call_once(ronce, [] {
+				for (auto &row : krw)
+					for (CK k : row) (void)hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+			});
+			if (h.K != 2 && h.K != 4 && h.K != 8) return fail(MBIK_EINVAL, "constraint_mode wave roles: 2, 4 or 8 roles");
+			ck = krw[h.has_chain ? 1 : 0][h.K == 2 ? 0 : h.K == 4 ? 1 : 2];
+			threads = 64 * h.K;
+		}
+		hipLaunchKernelGGL(ck, dim3((unsigned)((count + per_block - 1) / per_block)), dim3(threads), clds, stream, p->dev,
 				p->cm, first, count, pose_in, targets, pose_out, iterations, seg_lo, seg_hi);
 		hipError_t e = hipGetLastError();
 		if (e != hipSuccess) return fail(MBIK_EHIP, std::string("kernel launch failed: ") + hipGetErrorString(e));
@@ -3606,7 +3640,7 @@ int32_t mbik_plan_get_info(const mbik_plan *p, mbik_plan_info *o) {
 	o->segment_count = h.NS;
 	o->level_count = maxh + 1;
 	o->lanes_per_skeleton = h.K;
-	o->skeletons_per_block = h.constraint_mode ? 64 >> h.log2K : h.spw;
+	o->skeletons_per_block = h.constraint_mode ? (h.cm_roles ? cmode_shape_of(p, h.N).spw : 64 >> h.log2K) : h.spw;
 	o->max_headings = h.max_headings;
 	o->device = p->device;
 	o->device_bytes = p->device_bytes;
@@ -3624,7 +3658,7 @@ int32_t mbik_plan_get_info(const mbik_plan *p, mbik_plan_info *o) {
 	o->libm_variant = h.libm_variant;
 	o->helper_wave = helper_on(p) ? 1 : 0;
 	o->heading_slots = p->dev.prio_mask;
-	o->wave_roles = h.wave_roles;
+	o->wave_roles = h.wave_roles | h.cm_roles;
 	return MBIK_OK;
 }
 
@@ -3798,15 +3832,25 @@ static int cmode_autotune(mbik_plan *p, int first, int count, const float *pose_
 	}
 	int rc = copy(true);
 	float best_ms = 0.0f;
-	int best = 0, best_div = 0;
-	// lanes per skeleton x skeletons per wave (full waves, or half: twice the waves per SIMD
-	// for the node-cache misses to overlap)
-	for (int cand = 0; cand < 2 * 7 && rc == MBIK_OK; cand++) {
-		const int lanes = 1 << (cand >> 1), div = cand & 1;
-		if (lanes > max_lanes) break;
+	int best = 0, best_div = 0, best_rw = 0;
+	// classic: lanes per skeleton x skeletons per wave (full waves, or half: twice the waves per
+	// SIMD for the node-cache misses to overlap); wave roles (cmode.h mbik_cmode_kernel_rw, plans
+	// without stabilization, unless pinned off): 2, 4 or 8 roles x 64, 32 or 16 skeletons per block
+	const int roles0 = p->roles_override;
+	std::vector<std::array<int, 3>> cands; // lanes, spw div, wave roles
+	if (roles0 != 1)
+		for (int lanes = 1; lanes <= max_lanes && lanes <= 64; lanes <<= 1)
+			for (int div = 0; div < 2; div++) cands.push_back({lanes, div, 0});
+	if (roles0 != 0 && h.stabilization_passes == 0)
+		for (int lanes = 2; lanes <= std::min(8, std::max(2, max_lanes)); lanes <<= 1)
+			for (int div = 0; div < 3; div++) cands.push_back({lanes, div, 1});
+	for (size_t ci = 0; ci < cands.size() && rc == MBIK_OK; ci++) {
+		const int lanes = cands[ci][0], div = cands[ci][1];
 		p->cm_lanes = lanes;
 		p->cm_spw_div = div;
+		p->roles_override = cands[ci][2];
 		if ((rc = ensure_schedule(p, count)) != MBIK_OK) break;
+		if (cands[ci][2] && !h.cm_roles) continue; // (not eligible: 64-bit addressing)
 		float ms = 0.0f;
 		for (int r = 0; r < 3 && rc == MBIK_OK; r++) { // first run warms up, untimed
 			if ((rc = copy(false)) != MBIK_OK) break;
@@ -3822,6 +3866,7 @@ static int cmode_autotune(mbik_plan *p, int first, int count, const float *pose_
 			best_ms = ms;
 			best = lanes;
 			best_div = div;
+			best_rw = cands[ci][2];
 		}
 	}
 	if (rc == MBIK_OK) rc = copy(false);
@@ -3831,6 +3876,7 @@ static int cmode_autotune(mbik_plan *p, int first, int count, const float *pose_
 	(void)hipFree(save);
 	p->cm_lanes = best;
 	p->cm_spw_div = best_div;
+	p->roles_override = rc == MBIK_OK ? best_rw : roles0;
 	if (rc != MBIK_OK) return rc;
 	return ensure_schedule(p, count);
 }

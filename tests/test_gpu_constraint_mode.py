@@ -35,12 +35,14 @@ def animate(pose, rng, angle=0.2):
     return out
 
 
-def run_frames(oracle, wl, frames=4, stab=0, seed=0, lanes=0, spw=0):
+def run_frames(oracle, wl, frames=4, stab=0, seed=0, lanes=0, spw=0, roles=None, expect_roles=None):
     """Frame 1 starts from the setup pose; then the output is fed back (a still skeleton)
-    and, every other frame, animated."""
+    and, every other frame, animated.  roles: mbik_plan_set_wave_roles (None: the default)."""
     rng = np.random.default_rng(seed)
     ref_o = oracle.Oracle(wl, constraint_mode=True, stabilization_passes=stab)
     plan = Plan.from_workload(wl, constraint_mode=True, stabilization_passes=stab, lanes=lanes)
+    if roles is not None:
+        plan.set_wave_roles(roles)
     if spw:
         plan.set_layout(lanes, spw, 0)
     pose = wl.pose.copy()
@@ -51,6 +53,8 @@ def run_frames(oracle, wl, frames=4, stab=0, seed=0, lanes=0, spw=0):
         assert_parity(got, ref, f"frame {f}")
         changed += int((got[..., 0:4] != pose[..., 0:4]).any(-1).sum())
         pose = animate(ref, rng) if f % 2 else ref
+    if expect_roles is not None:
+        assert plan.info()["wave_roles"] == expect_roles
     plan.close()
     ref_o.close()
     return changed
