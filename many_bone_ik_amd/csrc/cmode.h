@@ -132,7 +132,7 @@ struct CmodeLane {
 		const int p = pre[b];
 		atomicOr(word(kind, p >> 5), 1u << (p & 31));
 	}
-	__device__ void mark_range(int kind, int a0, int z0) const { // positions [a0, z0)
+	__device__ __forceinline__ void mark_range(int kind, int a0, int z0) const { // positions [a0, z0)
 		for (int w = a0 >> 5; w <= ((z0 - 1) >> 5) && a0 < z0; w++) {
 			const int a = max(a0, w * 32) - w * 32, z = min(z0, w * 32 + 32) - w * 32; // bits [a, z)
 			const uint32_t m = (z == 32 ? ~0u : ((1u << z) - 1u)) & ~((1u << a) - 1u);
@@ -142,7 +142,7 @@ struct CmodeLane {
 	__device__ __forceinline__ bool owned(int b) const { return pre[b] >= lo && pre[b] < hi; }
 	// IKNode3D::_propagate_transform_changed on bone b's pose node (ik_node_3d.cpp:33-49): the
 	// node, its bone-direction child, and every node of the list bones below it.
-	__device__ void propagate(int b) const {
+	__device__ __forceinline__ void propagate(int b) const {
 		const int lo = pre[b], hi = lo + sub[b];
 		mark_range(CK_POSE, lo, hi);
 		mark_range(CK_BDIR, lo, hi);
@@ -606,13 +606,13 @@ __global__ __launch_bounds__(64 * kCmodeMaxWaves) void mbik_cmode_kernel(DevPlan
 // pending cleanings ([KW][4][64]) and the non-finite flags (64).  No stabilization.
 //
 // Rows with a SCHED_CMSPLIT segment (SCHED_COOP): each bone-step is three phases between two
-// block barriers -- the group's first wave reads the first effector (the reference's first
-// read, which cleans the chain every later read of the step starts from), then every wave of
-// the group reads its clusters of the other effectors (plan.cpp cm_split_groups: effectors
-// whose dirty chains overlap beyond the first one's path stay on one wave, in order), then the
-// first wave runs the rest of the step (the bone's own read, the swing and the twist).  The other
-// tasks of such a row run their whole step in the last phase.  Sibling segments touch disjoint
-// subtrees, and the first wave's writes reach the other waves through the barriers.
+// block barriers -- the group's first wave cleans the segment's trunk as the reference's first
+// effective read would, then every wave of the group reads its clusters of effectors
+// (plan.cpp cm_split_groups: effectors whose paths share a node below the trunk stay on one
+// wave, in order), then the first wave runs the rest of the step (the bone's own read, the swing
+// and the twist).  The other tasks of such a row run their whole step in the last phase.
+// Sibling segments touch disjoint subtrees, and a wave's writes reach the others through the
+// barriers.
 template <bool NB32, bool CHAIN, int KW>
 __global__ __launch_bounds__(64 * KW) void mbik_cmode_kernel_rw(DevPlan t, CmodeState c, int first, int count,
 		const float *__restrict__ pose_in, const float *__restrict__ targets, float *__restrict__ pose_out, int iterations,
@@ -685,36 +685,63 @@ __global__ __launch_bounds__(64 * KW) void mbik_cmode_kernel_rw(DevPlan t, Cmode
 			if constexpr (CHAIN)
 				while (r1 < t.nrows && (t.sched[r1 * K].w & mbik::SCHED_CHAIN)) r1++;
 			int p1 = -1, p2 = -1, p3 = -1;
-			if (task0.w & mbik::SCHED_COOP) {
-				// (a cooperative row is one row: packed levels have one-wave tasks only)
-				const int seg = task0.x, j = task0.y, m = task0.z;
-				const bool act = valid && seg >= 0 && seg >= seg_lo && seg <= seg_hi;
-				const bool split = (task0.w & mbik::SCHED_CMSPLIT) != 0;
-				const int nq = row_steps(t, r, seg_lo, seg_hi);
-				int k0 = 0, ns = 0, e0 = 0, e1 = 0;
-				if (seg >= 0) {
-					set_range(seg);
-					k0 = t.seg_bone_off[seg];
-					ns = t.seg_bone_off[seg + 1] - k0;
-					e0 = t.seg_eff_off[seg];
-					e1 = t.seg_eff_off[seg + 1];
-				}
-				for (int q = 0; q < nq; q++) {
-					const bool step = act && q < ns;
-					if (split && step && j == 0) C.bdir_touch(t.eff_bone[t.seg_effs[e0]]);
+			// One loop for both kinds of row, with one site each for the effector reads, the
+			// bone-step and the cleaning: every extra inlined copy of the node-cache code costs
+			// thousands of instructions.
+			//   cooperative row (SCHED_COOP): nq bone-steps of three phases between two block
+			//   barriers -- the group's first wave reads the first effector, the group's waves
+			//   read their clusters of the others, the first wave runs the rest of the step (the
+			//   row's other tasks run their whole step then);
+			//   other rows (one row, or a packed level): the wave's segments back to back.
+			const bool coop = (task0.w & mbik::SCHED_COOP) != 0;
+			const int j = task0.y;
+			const bool split = coop && (task0.w & mbik::SCHED_CMSPLIT) != 0;
+			const int nq = coop ? row_steps(t, r, seg_lo, seg_hi) : 0;
+			int seg = coop ? task0.x : -1, k = 0, ke = 0, rr = r - 1, q = 0;
+			if (coop && valid && seg >= 0 && seg >= seg_lo && seg <= seg_hi) {
+				set_range(seg);
+				k = t.seg_bone_off[seg];
+				ke = t.seg_bone_off[seg + 1];
+			}
+			const int e0 = seg >= 0 ? t.seg_eff_off[seg] : 0, e1 = seg >= 0 ? t.seg_eff_off[seg + 1] : 0;
+			for (;;) {
+				bool run;
+				if (coop) {
+					if (q >= nq) break;
+					const bool step = k + q < ke;
+					// Phase 0, the group's first wave: the trunk bone T (plan.cpp cm_split_groups)
+					// made clean the way the reference's reads clean it.  Only the first effector
+					// whose bone-direction cache is dirty walks (the earlier reads find their caches
+					// clean); if T is dirty and that walk runs through T, its part from T up is
+					// T's own chain -- recomputed here, the same nodes and values -- and the rest
+					// of the walk is left to phase 1.  A walk that would stop below T (rare: a
+					// clean node under a dirty T) leaves every read to this wave, in order.
+					if (split && step && j == 0) {
+						const int T = (t.seg_eff_grp[e0] >> 4) - 1;
+						int from = e0, seq = 0;
+						if (C.dirty(CK_POSE, T)) {
+							while (from < e1 && !C.dirty(CK_BDIR, t.eff_bone[t.seg_effs[from]])) from++;
+							if (from < e1) {
+								int x = t.eff_bone[t.seg_effs[from]];
+								while (x != T && C.dirty(CK_POSE, x)) x = t.bone_pose_parent[x];
+								if (x == T) (void)C.pose_global(T);
+								else seq = 1;
+							}
+						}
+						pv[role * 4 * 64 + lane] = from | seq << 16;
+					}
 					__syncthreads();
-					if (split && step)
-						for (int i = e0 + 1; i < e1; i++)
-							if (t.seg_eff_grp[i] == j) C.bdir_touch(t.eff_bone[t.seg_effs[i]]);
+					// Phase 1: each wave reads its clusters from there on, in order (or the first
+					// wave all of them, in order).
+					if (split && step) {
+						const int v = pv[(role - j) * 4 * 64 + lane], seq = v >> 16;
+#pragma nounroll
+						for (int i = v & 0xffff; i < e1; i++)
+							if (seq ? j == 0 : (t.seg_eff_grp[i] & 15) == j) C.bdir_touch(t.eff_bone[t.seg_effs[i]]);
+					}
 					__syncthreads();
-					if (step && j == 0) cmode_step<false, NB32>(C, seg, k0 + q, 0, 1, tg, nullptr, prev_dev, !split);
-				}
-			} else {
-				// rows r .. r1-1: one row, or a packed level run back to back by each wave (the
-				// classic kernel's CHAIN loop); a group of several waves without a split runs on
-				// its first wave
-				int rr = r - 1, k = 0, ke = 0, seg = 0;
-				for (;;) {
+					run = step && j == 0;
+				} else {
 					while (k >= ke && rr + 1 < r1) {
 						const int4 task = t.sched[++rr * K + role];
 						if (valid && task.x >= 0 && task.x >= seg_lo && task.x <= seg_hi && task.y == 0) {
@@ -731,9 +758,11 @@ __global__ __launch_bounds__(64 * KW) void mbik_cmode_kernel_rw(DevPlan t, Cmode
 						}
 					}
 					if (k >= ke) break;
-					cmode_step<false, NB32>(C, seg, k, 0, 1, tg, nullptr, prev_dev);
-					k++;
+					run = true;
 				}
+				if (run) cmode_step<false, NB32>(C, seg, coop ? k + q : k, 0, 1, tg, nullptr, prev_dev, !split);
+				if (coop) q++;
+				else k++;
 			}
 			// The cleaning the reference's first read above a segment root did, for every pending
 			// chain of the row (siblings share them; a chain is computed once and then clean): the
@@ -748,11 +777,11 @@ __global__ __launch_bounds__(64 * KW) void mbik_cmode_kernel_rw(DevPlan t, Cmode
 			if (wv == 0 && valid) {
 				C.lo = 0;
 				C.hi = 0x7fffffff;
-				for (int w = 0; w < K; w++)
-					for (int q = 0; q < 4; q++) {
-						const int x = pv[(w * 4 + q) * 64 + lane];
-						if (x >= 0) (void)C.pose_global(x);
-					}
+#pragma nounroll
+				for (int w = 0; w < 4 * K; w++) {
+					const int x = pv[w * 64 + lane];
+					if (x >= 0) (void)C.pose_global(x);
+				}
 			}
 			MBIK_PROF_T(rc1);
 			MBIK_PROF_ADD(8, rc0, rc1);

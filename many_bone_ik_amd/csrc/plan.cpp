@@ -585,15 +585,16 @@ static int ceil_log2(int v) {
 }
 
 // constraint_mode, wave roles: the split of a multi-effector segment's effector reads over its
-// group of m waves.  The reference reads the effectors in order, each read cleaning the dirty
-// chain above its effector.  After the first effector's read (alone), effectors a and b may be
-// read concurrently on separate waves only if every node they share -- the prefix of depth
-// lcp(a, b) of both paths from the root -- lies on the first effector's path, which that read
-// has cleaned: lcp(a, b) <= min(lcp(0, a), lcp(0, b)).  Effectors that fail this (transitively)
-// form a cluster that one wave reads in the reference's order; clusters go to waves longest
+// group of m waves (cmode.h mbik_cmode_kernel_rw).  The reference reads the effectors in order,
+// each read cleaning the dirty pose chain above its effector.  All of the segment's effector
+// paths from the root share a trunk down to the deepest common bone T (path length L).  Once T is
+// clean, a read never walks above T, so two effectors may be read concurrently on separate waves
+// if their paths share nothing below T (lcp(a, b) <= L); effectors that share more (transitively)
+// form a cluster that one wave reads in the reference's order.  Clusters go to waves longest
 // first.  A recomputed node's value does not depend on which read recomputes it (nothing above
 // the reads changes during them), so the caches end as after the sequential reads.
-// Writes seg_eff_grp for the segment; false when fewer than two clusters (no split).
+// seg_eff_grp[i]: the wave of effector i's cluster (bits 0-3); the segment's first entry also
+// holds T + 1 (bits 4 and up).  False (no split) with fewer than two clusters.
 static bool cm_split_groups(HostPlan &p, int sg, int m) {
 	const int e0 = p.seg_eff_off[sg], e1 = p.seg_eff_off[sg + 1], n = e1 - e0;
 	auto plen = [&](int a) { const int e = p.seg_effs[a]; return p.eff_path_off[e + 1] - p.eff_path_off[e]; };
@@ -604,24 +605,25 @@ static bool cm_split_groups(HostPlan &p, int sg, int m) {
 		while (l < la && l < lb && p.eff_path[p.eff_path_off[ea] + l] == p.eff_path[p.eff_path_off[eb] + l]) l++;
 		return l;
 	};
-	if (n > 256) return false; // (the pairwise test is quadratic; such segments run on one wave)
-	std::vector<int> l0(n, 0);
-	for (int a = 1; a < n; a++) l0[a] = lcp(e0, e0 + a);
-	std::vector<int> par(n); // clusters of effectors e0 + 1 .. : union over the pairs that fail the test
+	if (n < 2 || n > 256 || m > 16) return false; // (the pairwise test is quadratic; such segments run on one wave)
+	int L = plen(e0);
+	for (int a = 1; a < n; a++) L = std::min(L, lcp(e0, e0 + a));
+	if (L < 1) return false;
+	std::vector<int> par(n); // clusters: union over the pairs that share a node below T
 	for (int i = 0; i < n; i++) par[i] = i;
 	auto find = [&](int x) {
 		while (par[x] != x) x = par[x] = par[par[x]];
 		return x;
 	};
-	for (int a = 1; a < n; a++)
+	for (int a = 0; a < n; a++)
 		for (int b = a + 1; b < n; b++)
-			if (lcp(e0 + a, e0 + b) > std::min(l0[a], l0[b])) par[find(b)] = find(a);
+			if (lcp(e0 + a, e0 + b) > L) par[find(b)] = find(a);
 	std::vector<int> roots;
 	std::vector<int64_t> cost(n, 0);
-	for (int a = 1; a < n; a++) {
+	for (int a = 0; a < n; a++) {
 		const int r = find(a);
 		if (cost[r] == 0) roots.push_back(r);
-		cost[r] += std::max(1, plen(e0 + a) - l0[a]); // the nodes below the first path
+		cost[r] += std::max(1, plen(e0 + a) - L); // the nodes below T
 	}
 	if ((int)roots.size() < 2) return false;
 	std::stable_sort(roots.begin(), roots.end(), [&](int x, int y) { return cost[x] > cost[y]; });
@@ -634,8 +636,9 @@ static bool cm_split_groups(HostPlan &p, int sg, int m) {
 		wave[r] = w;
 		load[w] += cost[r];
 	}
-	for (int a = 1; a < n; a++) p.seg_eff_grp[e0 + a] = wave[find(a)];
-	p.seg_eff_grp[e0] = 0;
+	for (int a = 0; a < n; a++) p.seg_eff_grp[e0 + a] = wave[find(a)];
+	const int T = p.eff_path[p.eff_path_off[p.seg_effs[e0]] + L - 1];
+	p.seg_eff_grp[e0] |= (T + 1) << 4;
 	return true;
 }
 

@@ -1793,7 +1793,7 @@ __device__ void coop_walk(const DevPlan &t, int seg, int k, int j, int m, size_t
 // IKBone3D::set_skeleton_bone_pose (ik_bone_3d.cpp:170-179); returns whether the basis was
 // non-finite (and replaced by the identity, :174-176).
 template <bool SEL = false>
-__device__ bool write_pose(const X3 &t, float *out) {
+__device__ __forceinline__ bool write_pose(const X3 &t, float *out) {
 	B3 b = t.b;
 	const bool bad = !is_finite(b);
 	if (bad) b = bid();

@@ -54,9 +54,9 @@ def test_tight_limits_many_snaps(oracle, mbik):
 
 
 def test_shared_chains_stay_on_one_wave(oracle, mbik):
-    """A root segment whose effectors pair up below it (two limbs of two fingers each, the first
-    effector on a third limb): the fingers of one limb share that limb's dirty chain beyond the
-    first effector's path, so they are one cluster, read in order by one wave."""
+    """A root segment whose effectors pair up below it (two limbs of two fingers each, and a
+    third limb's tip): the fingers of one limb share that limb's dirty chain below the trunk (the
+    root bone), so they are one cluster, read in order by one wave (plan.cpp cm_split_groups)."""
     parents = [-1, 0, 1, 2, 3, 3, 0, 6, 7, 8, 8, 0, 11, 12]
     #          root, limb A 1-3, fingers 4 5; limb B 6-8, fingers 9 10; limb C 11-13 (tip 13)
     topo = W.custom_topology(parents, [13, 4, 5, 9, 10], list(range(1, 14)), cones_per_bone=1,
