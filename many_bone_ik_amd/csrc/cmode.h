@@ -697,8 +697,9 @@ __global__ __launch_bounds__(64 * KW) void mbik_cmode_kernel_rw(DevPlan t, Cmode
 			const int j = task0.y;
 			const bool split = coop && (task0.w & mbik::SCHED_CMSPLIT) != 0;
 			const int nq = coop ? row_steps(t, r, seg_lo, seg_hi) : 0;
+			// (the segment bookkeeping is wave-uniform; only the work is per lane, for valid lanes)
 			int seg = coop ? task0.x : -1, k = 0, ke = 0, rr = r - 1, q = 0;
-			if (coop && valid && seg >= 0 && seg >= seg_lo && seg <= seg_hi) {
+			if (coop && seg >= 0 && seg >= seg_lo && seg <= seg_hi) {
 				set_range(seg);
 				k = t.seg_bone_off[seg];
 				ke = t.seg_bone_off[seg + 1];
@@ -716,7 +717,7 @@ __global__ __launch_bounds__(64 * KW) void mbik_cmode_kernel_rw(DevPlan t, Cmode
 					// T's own chain -- recomputed here, the same nodes and values -- and the rest
 					// of the walk is left to phase 1.  A walk that would stop below T (rare: a
 					// clean node under a dirty T) leaves every read to this wave, in order.
-					if (split && step && j == 0) {
+					if (split && step && j == 0 && valid) {
 						const int T = (t.seg_eff_grp[e0] >> 4) - 1;
 						int from = e0, seq = 0;
 						if (C.dirty(CK_POSE, T)) {
@@ -733,7 +734,7 @@ __global__ __launch_bounds__(64 * KW) void mbik_cmode_kernel_rw(DevPlan t, Cmode
 					__syncthreads();
 					// Phase 1: each wave reads its clusters from there on, in order (or the first
 					// wave all of them, in order).
-					if (split && step) {
+					if (split && step && valid) {
 						const int v = pv[(role - j) * 4 * 64 + lane], seq = v >> 16;
 #pragma nounroll
 						for (int i = v & 0xffff; i < e1; i++)
@@ -744,7 +745,7 @@ __global__ __launch_bounds__(64 * KW) void mbik_cmode_kernel_rw(DevPlan t, Cmode
 				} else {
 					while (k >= ke && rr + 1 < r1) {
 						const int4 task = t.sched[++rr * K + role];
-						if (valid && task.x >= 0 && task.x >= seg_lo && task.x <= seg_hi && task.y == 0) {
+						if (task.x >= 0 && task.x >= seg_lo && task.x <= seg_hi && task.y == 0) {
 							if (pend >= 0) {
 								p3 = p2;
 								p2 = p1;
@@ -760,7 +761,7 @@ __global__ __launch_bounds__(64 * KW) void mbik_cmode_kernel_rw(DevPlan t, Cmode
 					if (k >= ke) break;
 					run = true;
 				}
-				if (run) cmode_step<false, NB32>(C, seg, coop ? k + q : k, 0, 1, tg, nullptr, prev_dev, !split);
+				if (run && valid) cmode_step<false, NB32>(C, seg, coop ? k + q : k, 0, 1, tg, nullptr, prev_dev, !split);
 				if (coop) q++;
 				else k++;
 			}
