@@ -1565,7 +1565,11 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, int xs
 	// bone-direction caches are refreshed from here on.
 	// Every lane of the group holds identical values, so each writes its own copy (same
 	// bytes) and later reads never depend on another lane's store ordering.
-	for (int c = sr.w & 0xffff, ce = c + (sr.w >> 16); c < ce; c++) SF[t.bone_child_effs[c]] = 0;
+	// (Without stabilization nothing reads those flags before the step's end, where the stores
+	// go instead: placed here, in device memory they were the stores the swing's and twist's
+	// table loads then waited for -- vmcnt counts stores too.)
+	if constexpr (STAB)
+		for (int c = sr.w & 0xffff, ce = c + (sr.w >> 16); c < ce; c++) SF[t.bone_child_effs[c]] = 0;
 	} else if (STAB && oe_mode == 1) {
 		// constraint_mode still builds the target headings before the loop (:135)
 		Headings H;
@@ -1638,6 +1642,8 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, int xs
 	}
 	{
 		L.st(b, Lb);
+		if constexpr (!STAB)
+			for (int c = sr.w & 0xffff, ce = c + (sr.w >> 16); c < ce; c++) SF[t.bone_child_effs[c]] = 0;
 		// A swing with no propagating twist leaves b's bone-direction cache stale until the
 		// parent's set_global_pose (IKNode3D::rotate_local_with_global, ik_node_3d.cpp:56-67).
 		if ((flags & mbik::BF_PINNED) && swung && !twist_changed) {
@@ -1742,11 +1748,47 @@ __device__ void global_pass_pipelined(const DevPlan &t, int seg, const LV &L, co
 	}
 }
 
+// The same with the globals in device memory (state placement 2), kGpGroup bones at a time: a
+// group's locals (and, first, the parent's checkpoint global) load together, one wait, then its
+// products and stores.  gfx9's vmcnt counts stores as well as loads, and with both pending a wait
+// can only be for all of them: in the pipelined pass every product waited for the previous
+// bone's store (~2,000 cycles on a busy chip) before its local.  Same products, same order.
+constexpr int kGpGroup = 4;
+constexpr unsigned kWaitVm0 = 0x0F70; // s_waitcnt vmcnt(0) expcnt(7) lgkmcnt(15): gfx9 encoding
+template <class LV, class GV>
+__device__ void global_pass_grouped(const DevPlan &t, int seg, const LV &L, const GV &G) {
+	const int kb = t.seg_bone_off[seg], kt = t.seg_bone_off[seg + 1] - 1;
+	const int pp = t.bone_pose_parent[t.seg_bones[kt]];
+	X3 Gprev;
+	for (int k = kt; k >= kb; k -= kGpGroup) {
+		X3 Lq[kGpGroup];
+#pragma unroll
+		for (int u = 0; u < kGpGroup; u++)
+			if (k - u >= kb) Lq[u] = L.ld(t.seg_bones[k - u]);
+		X3 Gp;
+		if (k == kt && pp >= 0) Gp = G.ld(t.bone_gslot[pp]);
+		__builtin_amdgcn_s_waitcnt(kWaitVm0);
+#pragma unroll
+		for (int u = 0; u < kGpGroup; u++) {
+			if (k - u < kb) break;
+			if (u == 0 && k == kt)
+				Gprev = pp >= 0 ? Gp * Lq[0] : (pp == mbik::POSE_PARENT_ORIGIN ? xid() * Lq[0] : Lq[0]);
+			else
+				Gprev = Gprev * Lq[u];
+			const int gs = t.bone_gslot[t.seg_bones[k - u]];
+			if (gs >= 0) G.st(gs, Gprev);
+		}
+	}
+}
+
 // Iteration-start globals of one segment, root -> tip (IKNode3D::get_global_transform): the
-// pipelined pass above (its products and stores, in the same order).
+// pipelined pass above (its products and stores, in the same order); placement 2 the grouped one.
 template <class LV, class GV>
 __device__ __forceinline__ void global_pass(const DevPlan &t, int seg, const LV &L, const GV &G) {
-	global_pass_pipelined(t, seg, L, G);
+	if constexpr (std::is_same_v<GV, GTiled<BPtr<float>>>)
+		global_pass_grouped(t, seg, L, G);
+	else
+		global_pass_pipelined(t, seg, L, G);
 }
 
 // Wave roles, cooperative segment (SCHED_XS): wave j of the segment's group of m waves walks the
