@@ -6,7 +6,7 @@
 #       the -m gpu tests, then optionally smoke() and bench lines          -> gpurun_out/$TAG/
 #   tools/evidence.sh final              TAG
 #       the whole suite, smoke(), the default bench line (C2) with its rocprofv3 kernel stats,
-#       and the autotuned C3 / C4 / C5 lines                               -> gpurun_out/$TAG/
+#       the autotuned C3 / C4 / C5 lines and the constraint_mode C5 / C2 lines -> gpurun_out/$TAG/
 #   tools/evidence.sh counters           TAG, CFGS="2 3 4 5", LAYOUTS="c:layout ..." (default: the bench's picks)
 #       FETCH_SIZE / WRITE_SIZE passes (tools/traffic_from_pmc.py -> profiles/traffic.json) and the
 #       VALU mix (tools/valu_mix.sh -> tools/mix_entry.py -> profiles/valu_mix.json) per config,
@@ -58,6 +58,7 @@ final)
   (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- \
     python3 $ROOT/bench.py --steps 20 --warmup 3 --no-cpu-baseline > $OUT/c2_prof_bench.json 2> $OUT/c2_prof.err) || { echo "rocprof failed"; exit 1; }
   for c in 3 4 5; do bench c${c}_bench --config $c --steps 10 --warmup 2 || exit 1; done
+  for c in 5 2; do bench c${c}_cmode_bench --config $c --constraint-mode --steps 10 --warmup 3 || exit 1; done
   echo "done $(date +%T)";;
 counters)
   declare -A LAY=([2]="4:16:1:1:0:1:1" [3]="4:16:4:4:1:2:0" [4]="4:16:1:4:2:2:0" [5]="8:8:1:4:2:2:0")
