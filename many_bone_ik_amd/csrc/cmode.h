@@ -33,7 +33,7 @@
 // element was its own dword load and a 16-skeleton group used half of each 128-B line.
 constexpr int kNodeTile = 16;
 #ifndef MBIK_CM_GROUP
-#define MBIK_CM_GROUP 4
+#define MBIK_CM_GROUP 2
 #endif
 constexpr int kChainGroup = MBIK_CM_GROUP; // dirty-chain nodes per load group (CmodeLane::pose_global)
 constexpr unsigned kWaitVmAll = 0x0F70;       // s_waitcnt vmcnt(0) expcnt(7) lgkmcnt(15): gfx9 encoding
