@@ -12,6 +12,8 @@
 #       VALU mix (tools/valu_mix.sh -> tools/mix_entry.py -> profiles/valu_mix.json) per config,
 #       then tools/replay_count.sh for C2's helper-wave layout (unless NO_REPLAY=1; needs
 #       build/abl/libmbik_replay.so)
+#   tools/evidence.sh kstats             TAG, KSTATS="name:bench args;..."
+#       rocprofv3 --kernel-trace --stats of pinned layouts                 -> gpurun_out/$TAG/<name>/
 #   tools/evidence.sh profile <tag> <cfg>
 #       tools/round_profile.sh (bench line, kernel stats, keyed PMC traffic), then the VALU mix
 #       of the layout that pass timed
@@ -80,10 +82,22 @@ counters)
     head -2 $OUT/replay.log
   fi
   echo "done $(date +%T)";;
+kstats)
+  # rocprofv3 kernel stats of pinned layouts (no autotune launches in the averages):
+  # KSTATS="name:bench args;..." (default: the round's C4 / C5 / C5 constraint_mode picks)
+  KS=${KSTATS:-"c4:--config 4 --layout 4:64:1:0:2:2:0:1;c5:--config 5 --layout 8:64:2:0:2:2:0:1;c5cm:--config 5 --constraint-mode --layout 8:64:1:1:0:1:0:1"}
+  mkdir -p $OUT
+  IFS=';' read -ra KA <<< "$KS"
+  for kv in "${KA[@]}"; do
+    n=${kv%%:*}; args=${kv#*:}
+    (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/$n -o run --output-format csv -- \
+      python3 $ROOT/bench.py $args --steps 10 --warmup 3 --no-cpu-baseline > $OUT/$n.json 2> $OUT/$n.err) || { echo "$n failed"; exit 1; }
+    echo "$n done"
+  done;;
 profile)
   T=$1; CFG=$2
   bash tools/round_profile.sh $T $CFG || exit 1
   bash tools/valu_mix.sh ${T}_mix $CFG $(python3 tools/layout_of.py gpurun_out/$T/bench.json);;
 *)
-  echo "usage: tools/evidence.sh call|final|counters|profile ..." >&2; exit 2;;
+  echo "usage: tools/evidence.sh call|final|counters|kstats|profile ..." >&2; exit 2;;
 esac
