@@ -2260,8 +2260,13 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(WPE, WP
 		int count, const float *__restrict__ pose_in, const float *__restrict__ targets, float *__restrict__ pose_out, int iterations,
 		int seg_lo, int seg_hi) {
 	static_assert(KW <= 4 * WPE, "a block's waves must fit the CU at this register budget");
-	solve_block<false, 2, WPE == 1, true, false, false, PM, KW>(t, xcd_block(), first, count, pose_in, targets, pose_out, iterations,
-			seg_lo, seg_hi);
+// (MBIK_RW_HOIST 1, a diagnostic build: the single-effector segments' effector rows hoisted out
+// of their bone-steps at two waves per SIMD; 121 VGPRs spill, 400 B of scratch: not shipped)
+#ifndef MBIK_RW_HOIST
+#define MBIK_RW_HOIST 0
+#endif
+	solve_block<false, 2, WPE == 1 || MBIK_RW_HOIST, true, false, false, PM, KW>(t, xcd_block(), first, count, pose_in, targets, pose_out,
+			iterations, seg_lo, seg_hi);
 }
 
 template <int PM>
