@@ -1,13 +1,17 @@
 """Builds libmbik.so in-tree for gfx950 (hipcc, no JIT cache, no pip install).
 
     python -m many_bone_ik_amd.build [--force]
+    python -m many_bone_ik_amd.build --variant OUT.so [-DNAME[=V] ...]   (diagnostic builds: tools/)
 
-The library is rebuilt whenever the SHA-256 of its inputs -- every source, every header
-under csrc/ and include/, and the compiler flags -- differs from the stamp written next to
-it (libmbik.so.sha256), so an edited header can never leave a stale kernel in place.
+Every translation unit (the kernel families k_*.hip, the host side host_*.cpp and plan.cpp)
+compiles to its own object in parallel, then one link.  The library is rebuilt whenever the
+SHA-256 of its inputs -- every source, every header under csrc/ and include/, and the compiler
+flags -- differs from the stamp written next to it (libmbik.so.sha256), so an edited header can
+never leave a stale kernel in place.
 """
 from __future__ import annotations
 
+import concurrent.futures
 import glob
 import hashlib
 import os
@@ -17,7 +21,10 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libmbik.so")
-SOURCES = ["solve.hip", "plan.cpp"]
+# kernel families first (the longest compiles start first)
+SOURCES = ["k_solve_w1.hip", "k_solve_w2.hip", "k_cmode.hip", "k_solve_rw.hip", "host_selftest.cpp", "k_aux.hip", "host_plan.cpp",
+           "host_topo_io.cpp", "host_autotune.cpp", "host_multi.cpp", "plan.cpp"]
+OBJ = os.path.join(HERE, "..", "build", "obj")
 STAMP = OUT + ".sha256"
 
 # -ffp-contract=off: every float op rounds separately, as the reference's x86 build does.
@@ -26,6 +33,7 @@ STAMP = OUT + ".sha256"
 # C2 unchanged; tools/ab_run.sh).
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-slp-vectorize",
          "-Wno-unused-result"]
+COMPILE = [f for f in FLAGS if f != "-shared"]
 
 
 def _inputs() -> list[str]:
@@ -50,16 +58,45 @@ def _stale() -> bool:
         return fh.read().strip() != source_hash()
 
 
+def _jobs() -> int:
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(int(os.environ.get("MAX_JOBS", "16")), n, len(SOURCES)))
+
+
+def compile_library(out: str, extra_flags=(), verbose: bool = False, csrc: str = CSRC) -> None:
+    """Compiles every translation unit of `csrc` (in parallel) and links them into `out`."""
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    tag = hashlib.sha256((" ".join(COMPILE + list(extra_flags)) + out + csrc).encode()).hexdigest()[:12]
+    odir = os.path.join(OBJ, tag)
+    os.makedirs(odir, exist_ok=True)
+
+    def one(src: str) -> str:
+        obj = os.path.join(odir, os.path.splitext(src)[0] + ".o")
+        cmd = [hipcc, *COMPILE, *extra_flags, "-c", os.path.join(csrc, src), "-o", obj]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"compiling {src} failed:\n{r.stderr}")
+        return obj
+
+    with concurrent.futures.ThreadPoolExecutor(_jobs()) as ex:
+        objs = list(ex.map(one, SOURCES))
+    cmd = [hipcc, *FLAGS, *extra_flags, *objs, "-o", out + ".tmp"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(out + ".tmp", out)
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not _stale():
         return OUT
-    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    cmd = [hipcc, *FLAGS, *[os.path.join(CSRC, f) for f in SOURCES], "-o", OUT + ".tmp"]
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
     digest = source_hash()
-    subprocess.run(cmd, check=True)
-    os.replace(OUT + ".tmp", OUT)
+    compile_library(OUT, verbose=verbose)
     with open(STAMP, "w") as fh:
         fh.write(digest + "\n")
     return OUT
@@ -92,5 +129,17 @@ def build_capi_frame(verbose: bool = False) -> str:
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
-    print(build_capi_frame(verbose=True))
+    if "--variant" in sys.argv:
+        # a diagnostic build of the same sources with extra flags, e.g. -DMBIK_PROF (tools/)
+        # (--csrc DIR: the sources of another revision, tools/ab_build.sh)
+        args = sys.argv[sys.argv.index("--variant") + 1:]
+        src = CSRC
+        if "--csrc" in args:
+            j = args.index("--csrc")
+            src = os.path.abspath(args[j + 1])
+            del args[j:j + 2]
+        compile_library(os.path.abspath(args[0]), args[1:], verbose=True, csrc=src)
+        print(args[0])
+    else:
+        print(build(force="--force" in sys.argv, verbose=True))
+        print(build_capi_frame(verbose=True))

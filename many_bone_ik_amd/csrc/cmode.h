@@ -1,6 +1,6 @@
 // constraint_mode (ManyBoneIK3D::constraint_mode, ik_bone_segment_3d.cpp:142): every bone-step
-// skips the QCP fit and only applies the Kusudama swing and twist snaps.  Included by
-// solve.hip inside its anonymous namespace (DevPlan and the device helpers).
+// skips the QCP fit and only applies the Kusudama swing and twist snaps.  Device code of
+// k_cmode.hip (DevPlan and the device helpers from bone_step.h).
 //
 // Without the fit's set_global_pose nothing refreshes the IKNode3D tree as a whole, so the
 // result depends on which cached globals are stale:
@@ -25,35 +25,22 @@
 // the reference does at the first such read is applied after the row, one lane at a time.
 // Dirty words are shared by the skeleton's lanes: updates are LDS atomics.
 
-// The node state is skeleton-tiled like the default kernel's locals (LocTiled):
-// [N/16][slot][3 quads][16 skeletons][4], element f of node slot k of skeleton s at node_at(),
-// so one node of 16 consecutive skeletons is 768 contiguous bytes and a lane reads its node as
-// three 16-byte quads -- a wave's lane group (consecutive skeletons, one slot) reads 256
-// contiguous bytes per load instruction.  With the plain [slot][12][N] rows (round 2) every
-// element was its own dword load and a 16-skeleton group used half of each 128-B line.
-constexpr int kNodeTile = 16;
+#pragma once
+#include "solve_block.h"
+
+namespace {
+
+using mbik::CmodeState;
+using mbik::kCmodeMaxWaves;
+using mbik::kNodeTile;
+using mbik::node_area_floats;
+using mbik::node_at;
+
 #ifndef MBIK_CM_GROUP
 #define MBIK_CM_GROUP 2
 #endif
 constexpr int kChainGroup = MBIK_CM_GROUP; // dirty-chain nodes per load group (CmodeLane::pose_global)
 constexpr unsigned kWaitVmAll = 0x0F70;       // s_waitcnt vmcnt(0) expcnt(7) lgkmcnt(15): gfx9 encoding
-__host__ __device__ __forceinline__ size_t node_at(int slots, size_t s, int k, int f) {
-	return ((s / kNodeTile) * (size_t)slots + (size_t)k) * (12 * kNodeTile) + (size_t)(f >> 2) * (4 * kNodeTile) +
-			(s % kNodeTile) * 4 + (f & 3);
-}
-__host__ __device__ __forceinline__ size_t node_area_floats(int slots, size_t N) { return (N + kNodeTile - 1) / kNodeTile * kNodeTile * (size_t)slots * 12; }
-
-struct CmodeState {
-	float *node;        // node_at(): slots pose local (B), pose global (B), bone-direction global (B),
-	                    // constraint-orientation global (NC), twist global (NC)
-	uint32_t *dirty;    // [kind * W + word][N], kinds: pose, bone direction, orientation, twist
-	const int *pre;     // [B] pre-order position in the pose-node forest (list bones)
-	const int *sub;     // [B] subtree size
-	int W;              // dirty words per kind
-	int maxd;           // deepest pose chain
-	int spw = 0;        // skeletons per wave (<= 64 / K; fewer leave lanes idle but put more waves per SIMD)
-	int wpb = 1;        // waves per block: they share the block's LDS copy of the topology
-};
 
 enum { CK_POSE = 0, CK_BDIR = 1, CK_COR = 2, CK_CTW = 3 };
 
@@ -407,7 +394,6 @@ __device__ __forceinline__ void cmode_step(const CmodeLane<NB32> &C, int seg, in
 // staging it through LDS was measured slower (one lane per skeleton: C2 5.6 vs 5.1 ms, C5
 // 1003 vs 56 ms; LDS caps how many skeletons are resident;
 // profiles/r01_cmode_layout_sweep.jsonl).
-constexpr int kCmodeMaxWaves = 4; // waves per constraint_mode block (launch bound)
 // CHAIN: the schedule has packed levels (SCHED_CHAIN rows); plans without them keep the plain
 // row loop (its registers: the packed loop measured +2 % on C2).
 template <bool STAB, bool NB32, bool CHAIN = false>
@@ -833,3 +819,4 @@ __global__ __launch_bounds__(64) void mbik_cmode_reset_kernel(DevPlan t, CmodeSt
 	}
 	for (int w = 0; w < 4 * c.W; w++) c.dirty[(size_t)w * t.N + s] = ~0u;
 }
+} // namespace

@@ -560,11 +560,11 @@ int32_t state_floats_per_skeleton(const HostPlan &p) {
 	return p.B * 12 + p.n_gck * 12 + p.P * 25 + p.hs_floats + (p.stabilization_passes > 0 ? p.P * 10 : 0);
 }
 
-// Upper bound of the LDS bytes taken by the topology blob (solve.hip: upload_topology).
+// Upper bound of the LDS bytes taken by the topology blob (host_plan.cpp: upload_topology).
 int64_t topology_bytes(const HostPlan &p) {
 	int64_t w = 4 * (int64_t)p.sched.size() + 4;
 	auto ints = [&](size_t n) { w += (int64_t)std::max<size_t>(n, 1) + 1; };
-	// the tables MBIK_TOPO_TABLES lists (solve.hip), in its order
+	// the tables MBIK_TOPO_TABLES lists (kernels.h), in its order
 	ints(p.bone_pose_parent.size()); ints(p.bone_flags.size()); ints(p.bone_pin.size());
 	ints(p.bone_cons.size()); ints(p.bone_child_effs.size());
 	ints(p.seg_bone_off.size()); ints(p.seg_bones.size()); ints(p.seg_eff_off.size()); ints(p.seg_effs.size());
@@ -780,7 +780,7 @@ void build_schedule(HostPlan &p, int32_t lanes, int64_t nlaunch, int32_t spw_ove
 			p.nrows++;
 		}
 	}
-	// Staged-heading area (solve.hip, segments solved by several lanes of a row): 12 floats per
+	// Staged-heading area (bone_step.h, segments solved by several lanes of a row): 12 floats per
 	// heading plus 24 for the exchanged sums.  A translating split-exchange segment (staging 4 /
 	// 5, state placement 2) keeps there instead the effector globals its lanes built in the centroid pass, 12
 	// floats per lane and round, so that the sums pass rebuilds their headings without walking

@@ -1,5 +1,5 @@
 // Per-skeleton plan setup, shared by the host builder (plan.cpp) and the GPU builder
-// (solve.hip: mbik_setup_kernel): the bone-direction frames and the Kusudama frames that
+// (k_aux.hip: mbik_setup_kernel): the bone-direction frames and the Kusudama frames that
 // ManyBoneIK3D::_bone_list_changed derives from a skeleton's setup pose, cones and twist
 // (IKBone3D::update_default_bone_direction_transform ik_bone_3d.cpp:57-93,
 //  IKLimitCone3D::update_tangent_handles ik_open_cone_3d.cpp:36-120, IKRay3D

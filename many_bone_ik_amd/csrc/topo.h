@@ -1,6 +1,6 @@
 // GPU-side topology build: ManyBoneIK3D::_bone_list_changed's
 // segmentation and heading weights for one rig, written allocation-free and recursion-free so
-// that one GPU thread builds one rig (solve.hip: mbik_topology_kernel, a crowd of distinct rigs
+// that one GPU thread builds one rig (k_aux.hip: mbik_topology_kernel, a crowd of distinct rigs
 // at once).  It restates, table for table, what plan.cpp's build_topology computes on the host:
 //   IKBoneSegment3D::generate_default_segments    ik_bone_segment_3d.cpp:352-427 (preorder
 //                                                  segment creation, _create_next_bone :401-407)

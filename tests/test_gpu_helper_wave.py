@@ -12,7 +12,7 @@ from many_bone_ik_amd.solver import Plan
 from .test_gpu_parity import assert_parity
 
 pytestmark = pytest.mark.gpu
-RING_BYTES = 4 * 18 * 64 * 16 + 32   # solve.hip: kHelpRingBytes (kHelpSlots x kHelpF4 float4 per lane + counters)
+RING_BYTES = 4 * 18 * 64 * 16 + 32   # csrc/kernels.h: kHelpRingBytes (kHelpSlots x kHelpF4 float4 per lane + counters)
 
 
 def _helper_fits(info):

@@ -11,7 +11,5 @@ OUTDIR=${OUTDIR:-build/abl}
 mkdir -p $OUTDIR
 for tag in ${@:-CONVERT SLERP SWING TWIST}; do
   [ -n "${BIT[$tag]}" ] || { echo "unknown ablation $tag" >&2; exit 2; }
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off -fno-slp-vectorize -Wno-unused-result \
-    -DMBIK_ABLATE=${BIT[$tag]} many_bone_ik_amd/csrc/solve.hip many_bone_ik_amd/csrc/plan.cpp -o $OUTDIR/libmbik_abl_$tag.so &
+  python3 -m many_bone_ik_amd.build --variant $OUTDIR/libmbik_abl_$tag.so -DMBIK_ABLATE=${BIT[$tag]} >/dev/null
 done
-wait

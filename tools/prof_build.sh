@@ -6,8 +6,6 @@
 set -e
 cd "$(dirname "$0")/.."
 mkdir -p build/abl
-FLAGS=$(python3 -c "from many_bone_ik_amd.build import FLAGS; print(' '.join(FLAGS))")
 if [ "$1" = "REPLAY" ]; then DEF=-DMBIK_REPLAY; OUT=${OUT:-build/abl/libmbik_replay.so}; else DEF=-DMBIK_PROF; OUT=${OUT:-build/abl/libmbik_abl_PROF.so}; fi
 mkdir -p "$(dirname "$OUT")"
-/opt/rocm/bin/hipcc $FLAGS $DEF many_bone_ik_amd/csrc/solve.hip many_bone_ik_amd/csrc/plan.cpp -o $OUT
-echo $OUT
+python3 -m many_bone_ik_amd.build --variant $OUT $DEF

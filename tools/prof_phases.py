@@ -9,7 +9,7 @@ from many_bone_ik_amd.solver import Plan
 
 NAMES = ["load", "headings_qcp", "clamp_slerp_rotate", "swing", "twist", "global_pass", "store", "total",
          "step_start", "eff_headings", "qcp_adjugate", "convert_clamp", "slerp", "translate_steps", "qcp_centroid_sums", "tr_headings_build", "tr_staged_sums", "tr_rotate", "help_wait", "help_wait_b", "help_wait_first", "helper_global_pass", "helper_first_record"]
-# wave roles (ROLES=1): counters 18-23 are the cooperative rows' (solve.hip)
+# wave roles (ROLES=1): counters 18-23 are the cooperative rows' (solve_block.h)
 NAMES_RW = NAMES[:18] + ["rw_plain_rows", "rw_coop_walk", "rw_coop_sums", "rw_coop_barrier_wait", "rw_coop_steps", "rw_coop_rows"]
 dev = torch.device('cuda', 0)
 L = _lib.load()

@@ -6,9 +6,8 @@
 set -e
 cd "$(dirname "$0")/../.."
 mkdir -p build/san
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O1 -g -std=c++17 -fPIC -shared -ffp-contract=off -fno-slp-vectorize \
-  -Wno-unused-result -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-omit-frame-pointer \
-  -shared-libsan many_bone_ik_amd/csrc/solve.hip many_bone_ik_amd/csrc/plan.cpp -o build/san/libmbik_asan.so
+python3 -m many_bone_ik_amd.build --variant build/san/libmbik_asan.so -O1 -g -Xarch_host -fsanitize=address \
+  -Xarch_host -fsanitize=undefined -Xarch_host -fno-omit-frame-pointer -shared-libsan
 RT=$(ls /opt/rocm/lib/llvm/lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so | head -1)
 MBIK_LIB_OVERRIDE=$PWD/build/san/libmbik_asan.so LD_PRELOAD="$RT${LD_PRELOAD:+ $LD_PRELOAD}" \
   ASAN_OPTIONS=detect_leaks=0:halt_on_error=1 UBSAN_OPTIONS=halt_on_error=1:print_stacktrace=1 \

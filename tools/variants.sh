@@ -1,13 +1,11 @@
 #!/bin/bash
 # Timing variants of the solve library: tools/variants.sh TAG:"-DFLAG ..." ... -> build/abl/libmbik_abl_TAG.so
-# (built in parallel; time them with tools/ab_run.sh / tools/variant_run.sh on the GPU box)
+# (each build's translation units compile in parallel; time them with tools/ab_run.sh / tools/variant_run.sh on the GPU box)
 set -e
 cd "$(dirname "$0")/.."
 mkdir -p build/abl
 for spec in "$@"; do
   tag=${spec%%:*}; flags=${spec#*:}
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off -fno-slp-vectorize -Wno-unused-result \
-    $flags many_bone_ik_amd/csrc/solve.hip many_bone_ik_amd/csrc/plan.cpp -o build/abl/libmbik_abl_$tag.so 2>build/abl/$tag.log &
+  python3 -m many_bone_ik_amd.build --variant build/abl/libmbik_abl_$tag.so $flags >build/abl/$tag.log 2>&1
 done
-wait
 ls -la build/abl/*.so
