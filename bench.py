@@ -14,7 +14,12 @@ with its status.  Every rank solves its own contiguous shard of skeletons with n
 collective on the data path:
   --scaling weak    (default) the config's skeletons_per_gpu on every rank;
   --scaling strong  the config's whole batch (C4: 262,144) split by dist.shard_range.
-The RCCL gathers of the output poses are timed separately after the solve loop.
+The RCCL gathers of the output poses are timed separately after the solve loop.  At N > 1
+rank 0 then also times the library's own multi-GPU path (mbik_multi_solve: one process, one
+plan per visible device, peer-copy scatter / gather to device 0) over the whole batch while the
+other ranks wait on the host; it is reported under "library_multi", never as `value`.
+(--library-multi-devices 0,0 runs that measurement at N = 1 with the listed devices' plans:
+the one-GPU test of the same code.)
 
 --dry-run exercises the launcher / rendezvous / sharding / timing plumbing on CPU (gloo,
 no GPU, no solve): the tests use it, its line says "dry_run": true and is never a result.
@@ -62,6 +67,8 @@ def parse():
     ap.add_argument("--constraint-mode", action="store_true",
                     help="ManyBoneIK3D::constraint_mode (snaps only; each step is one frame of the persistent node caches)")
     ap.add_argument("--stabilization-passes", type=int, default=0)
+    ap.add_argument("--library-multi-devices", default="",
+                    help="comma-separated devices for the library_multi measurement (default at N > 1: 0..N-1)")
     ap.add_argument("--traffic-json", default=os.path.join(HERE, "profiles", "traffic.json"))
     ap.add_argument("--valu-mix-json", default=os.path.join(HERE, "profiles", "valu_mix.json"))
     return ap.parse_args()
@@ -157,6 +164,8 @@ def main():
         import torch.distributed as dist_mod
         dist = dist_mod
         dist.init_process_group(backend, device_id=torch.device("cuda", local_rank))
+        # a host-only group: the other ranks wait on it while rank 0 drives every GPU (library_multi)
+        host_group = dist.new_group(backend="gloo")
     dev = torch.device("cuda", local_rank)
 
     from many_bone_ik_amd import workloads as W
@@ -232,27 +241,49 @@ def main():
         pcie = {"ms_per_frame": hms, "skeletons_per_s": n / (hms * 1e-3),
                 "note": "mbik_solve_host: pageable host pose/targets in, solve, poses out"}
 
-    # parity spot check of this rank's first skeletons against the oracle (not timed)
+    # parity spot check against the oracle (not timed): this rank's first 32 and last 32
+    # skeletons, so the largest per-skeleton offsets of the timed launch are checked too
     parity = None
     if not args.no_parity and rank == 0:
         try:
             from oracle import pyoracle as po
-            k = min(64, n)
-            sub = W.generate(cfg, k, first=first)
-            o = po.Oracle(sub, **flags)
-            ref = o.solve(sub.pose, sub.targets, threads=16)
-            if args.constraint_mode:  # frames advance the node caches: compare a fresh first frame
-                sp = Plan.from_workload(sub, device=local_rank, **flags)
-                got = sp.solve_host(sub.pose, sub.targets)
-                sp.close()
-            else:
-                got = pose_out[:k].cpu().numpy()
+            head = min(32, n)
+            tail = min(32, n - head)
+            windows = [(0, head)] + ([(n - tail, tail)] if tail else [])
+            gots, refs = [], []
+            for lo, k in windows:
+                sub = W.generate(cfg, k, first=first + lo)
+                o = po.Oracle(sub, **flags)
+                refs.append(o.solve(sub.pose, sub.targets, threads=16))
+                o.close()
+                if args.constraint_mode:  # frames advance the node caches: compare a fresh first frame
+                    sp = Plan.from_workload(sub, device=local_rank, **flags)
+                    gots.append(sp.solve_host(sub.pose, sub.targets))
+                    sp.close()
+                else:
+                    gots.append(pose_out[lo:lo + k].cpu().numpy())
+            got, ref = np.concatenate(gots), np.concatenate(refs)
             qe = quat_error(got, ref)
-            parity = {"skeletons": k, "max_quat_err": float(qe.max()),
+            parity = {"skeletons": int(got.shape[0]), "ranges": [[first + lo, first + lo + k] for lo, k in windows],
+                      "max_quat_err": float(qe.max()),
                       "frac_skeletons_le_1e-4": float(np.mean(qe.max(-1) <= 1e-4)),
                       "bitwise_equal": bool(np.array_equal(got.view(np.uint32), ref.view(np.uint32)))}
         except Exception as e:  # oracle missing on the box: report, never fall back
             parity = {"error": str(e)}
+
+    # the library's single-process multi-GPU path (mbik_multi_*), after everything above
+    lib_multi = None
+    lm_devices = [int(x) for x in args.library_multi_devices.split(",") if x] or (list(range(world)) if world > 1 else [])
+    if lm_devices and not args.constraint_mode:
+        if dist:
+            dist.barrier(group=host_group)
+        if rank == 0:
+            try:
+                lib_multi = library_multi(cfg, [total // len(lm_devices)] * len(lm_devices), lm_devices, args, info, flags)
+            except Exception as e:  # noqa: BLE001 -- measurement only: reported, never part of `value`
+                lib_multi = {"error": f"{type(e).__name__}: {e}"}
+        if dist:
+            dist.barrier(group=host_group)
 
     if rank != 0:
         if dist:
@@ -346,6 +377,8 @@ def main():
         "pcie_inclusive": pcie,
         "parity": parity,
     }
+    if lib_multi is not None:
+        out["library_multi"] = lib_multi
     if world > 1:
         out["backend"] = backend
     if os.environ.get("MBIK_BENCH_DEVICE"):
@@ -358,6 +391,84 @@ def main():
     print(json.dumps(out))
     if dist:
         dist.destroy_process_group()
+
+
+def pin_layout(plan, info: dict) -> None:
+    """Pins a plan to the launch layout another plan's mbik_plan_info reports."""
+    plan.set_helper_wave(info["helper_wave"])
+    plan.set_wave_roles(info["wave_roles"])
+    plan.set_layout(info["lanes_per_skeleton"], info["skeletons_per_block"], info["checkpoint_interval"])
+    plan.set_heading_staging(info["heading_staging"])
+    plan.set_locals_placement(info["state_placement"])
+    plan.set_waves_per_simd(info["waves_per_simd"])
+
+
+def library_multi(cfg: int, counts, devices, args, info: dict, flags: dict) -> dict:
+    """SURVEY §8(e) through the library alone, as a single-process engine (Godot) would drive it:
+    one plan per device in `devices` (plan i owns skeletons [sum(counts[:i]), +counts[i]) of one
+    batch), mbik_multi_solve with the whole batch's inputs and outputs on device 0 -- the shards
+    go to their devices by peer copies, solve, and the poses come back by peer copies (no
+    collective).  Each plan runs the layout the timed rank-0 plan chose.  Times `args.steps`
+    frames after `args.warmup`, on device 0's stream (wall clock with a synchronize on both
+    sides, and HIP events), and checks the gathered poses' first and last skeletons against the
+    oracle."""
+    import torch
+    from many_bone_ik_amd import workloads as W
+    from many_bone_ik_amd.solver import Multi, Plan, quat_error
+    total = int(sum(counts))
+    t_gen = time.perf_counter()
+    wl = W.generate(cfg, total)
+    gen_s = time.perf_counter() - t_gen
+    plans, lo = [], 0
+    for d, c in zip(devices, counts):
+        p = Plan(wl.topo.parents, wl.pins(), wl.constraints(), wl.pose[lo:lo + c], wl.cones[lo:lo + c], wl.twist[lo:lo + c],
+                 iterations=wl.topo.iterations, default_damp=wl.default_damp, max_cones=wl.cones.shape[2], device=d, **flags)
+        pin_layout(p, info)
+        plans.append(p)
+        lo += c
+    m = Multi(plans, root_device=0)
+    root = torch.device("cuda", 0)
+    pi = torch.from_numpy(wl.pose).to(root)
+    tg = torch.from_numpy(wl.targets).to(root)
+    po = torch.empty_like(pi)
+    st = torch.cuda.Stream(root)
+    for _ in range(max(1, args.warmup)):
+        m.solve(pi.data_ptr(), tg.data_ptr(), po.data_ptr(), st.cuda_stream)
+    for d in sorted(set(devices)):
+        torch.cuda.synchronize(torch.device("cuda", d))
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(st)
+    for _ in range(args.steps):
+        m.solve(pi.data_ptr(), tg.data_ptr(), po.data_ptr(), st.cuda_stream)
+    e1.record(st)
+    st.synchronize()
+    wall = (time.perf_counter() - t0) / args.steps
+    ev_ms = e0.elapsed_time(e1) / args.steps
+    out = {"devices": devices, "skeletons": total, "plans": len(plans), "steps": args.steps,
+           "ms_per_frame": wall * 1e3, "event_ms_per_frame": ev_ms, "skeletons_per_s": total / wall,
+           "layout": {k: info[k] for k in ("lanes_per_skeleton", "skeletons_per_block", "checkpoint_interval", "heading_staging",
+                                           "state_placement", "waves_per_simd", "helper_wave", "wave_roles")},
+           "generate_s": gen_s,
+           "note": "mbik_multi_solve (one process, plan per device, peer-copy scatter/gather to device 0); "
+                   "a separate measurement, never `value`"}
+    if not args.no_parity:
+        from oracle import pyoracle as po_
+        got_all = po.cpu().numpy()
+        checks = []
+        for a, k in ((0, min(16, total)), (max(0, total - 16), min(16, total))):
+            sub = W.generate(cfg, k, first=a)
+            o = po_.Oracle(sub, **flags)
+            ref = o.solve(sub.pose, sub.targets, threads=16)
+            o.close()
+            got = got_all[a:a + k]
+            checks.append({"range": [a, a + k], "max_quat_err": float(quat_error(got, ref).max()),
+                           "bitwise_equal": bool(np.array_equal(got.view(np.uint32), ref.view(np.uint32)))})
+        out["parity"] = checks
+    m.close()
+    for p in plans:
+        p.close()
+    return out
 
 
 def layout_key(info: dict) -> str:

@@ -379,7 +379,10 @@ int32_t mbik_multi_create(mbik_plan *const *plans, int32_t n_plans, int32_t root
  * queued after the call sees the gathered poses.  Shards whose plan lives on the root device
  * solve in place in the caller's buffers (unless MBIK_MULTI_STAGE_ALL).  Calls on one handle are
  * ordered by root_stream; use one root stream per handle.  Returns the first error; a helper-wave
- * timeout of any plan is reported as by mbik_solve. */
+ * timeout of any plan is reported as by mbik_solve.  Shards run in plan order and the first
+ * failing shard ends the call: pose_out is then defined only for the shards before it, and
+ * root_stream still waits for everything the call queued (so the buffers are free to reuse once
+ * root_stream reaches that point). */
 int32_t mbik_multi_solve(mbik_multi *multi, const float *pose_in, const float *targets, float *pose_out, void *root_stream);
 /* The batch size (the plans' skeleton counts summed) and shard offsets (off[n_plans + 1],
  * may be NULL). */

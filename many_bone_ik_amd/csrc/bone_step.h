@@ -55,16 +55,17 @@ __device__ __forceinline__ void help_give_up(int *hfl, bool &stuck) {
 // t0: when the counter was last seen to move; tl: the previous poll.  Polls come every s_sleep
 // (microseconds apart), so a gap between two polls of more than timeout / 200 (10 ms of the 2 s
 // deadline) means the waves were suspended (preemption, context save/restore), not that the
-// partner stalled: the deadline restarts instead of counting the gap.
+// partner stalled: the gap is not counted (t0 moves forward by it), the rest of the wait is.  So
+// a stalled partner is still detected however often the waves are suspended.
 __device__ __forceinline__ bool help_expired(uint64_t &t0, uint64_t &tl, int &seen, int now_val, uint64_t timeout) {
 	const uint64_t now = (uint64_t)wall_clock64();
-	const bool resumed = t0 != 0 && now - tl > timeout / 200;
-	tl = now;
-	if (t0 == 0 || now_val != seen || resumed) {
-		t0 = now;
+	if (t0 == 0 || now_val != seen) {
+		t0 = tl = now;
 		seen = now_val;
 		return false;
 	}
+	if (now - tl > timeout / 200) t0 += now - tl;
+	tl = now;
 	return now - t0 > timeout;
 }
 __device__ __forceinline__ void help_wait(int *hfl, int k, int v, bool &stuck, uint64_t timeout) {

@@ -9,6 +9,34 @@
 
 using namespace mbik_host;
 
+namespace {
+// The layout settings a caller may pin, and what an autotune may change.  An autotune that fails,
+// or that times nothing (no eligible candidate), leaves them as the caller set them.
+struct Overrides {
+	int lanes, spw, interval, staging, locals, waves, helper, roles, cm_lanes, cm_spw_div;
+};
+Overrides save_overrides(const mbik_plan *p) {
+	return Overrides{p->lanes_override, p->spw_override, p->interval_override, p->staging_override, p->locals_override,
+			p->waves_override, p->helper_override, p->roles_override, p->cm_lanes, p->cm_spw_div};
+}
+void restore_overrides(mbik_plan *p, const Overrides &o) {
+	p->lanes_override = o.lanes;
+	p->spw_override = o.spw;
+	p->interval_override = o.interval;
+	p->staging_override = o.staging;
+	p->locals_override = o.locals;
+	p->waves_override = o.waves;
+	p->helper_override = o.helper;
+	p->roles_override = o.roles;
+	p->cm_lanes = o.cm_lanes;
+	p->cm_spw_div = o.cm_spw_div;
+	p->sched_K = -1;
+}
+constexpr int kNothingTimed = 1; // (internal: no candidate was eligible)
+} // namespace
+static int autotune_layouts(mbik_plan *p, int first, int count, const float *pose_in, const float *targets, float *pose_out,
+		hipStream_t st);
+
 extern "C" {
 
 // constraint_mode: every solve advances the persistent node caches (a frame), so the caches
@@ -83,10 +111,11 @@ static int cmode_autotune(mbik_plan *p, int first, int count, const float *pose_
 	(void)hipEventDestroy(e0);
 	(void)hipEventDestroy(e1);
 	(void)hipFree(save);
+	if (rc != MBIK_OK) return rc;
+	if (best == 0) return kNothingTimed;
 	p->cm_lanes = best;
 	p->cm_spw_div = best_div;
-	p->roles_override = rc == MBIK_OK ? best_rw : roles0;
-	if (rc != MBIK_OK) return rc;
+	p->roles_override = best_rw;
 	return ensure_schedule(p, count);
 }
 
@@ -136,7 +165,30 @@ int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const flo
 	}
 	DeviceGuard guard(p->device);
 	hipStream_t st = reinterpret_cast<hipStream_t>(hip_stream);
-	if (p->host.constraint_mode) return cmode_autotune(p, first, count, pose_in, targets, pose_out, st);
+	const Overrides o0 = save_overrides(p);
+	int rc = p->host.constraint_mode ? cmode_autotune(p, first, count, pose_in, targets, pose_out, st)
+									 : autotune_layouts(p, first, count, pose_in, targets, pose_out, st);
+	if (rc == kNothingTimed) {
+		// nothing eligible was timed (e.g. wave roles pinned on a plan that cannot have them):
+		// the caller's settings stand
+		restore_overrides(p, o0);
+		return ensure_schedule(p, count);
+	}
+	if (rc != MBIK_OK) {
+		// a candidate failed: the plan goes back to the caller's settings, and the error stands
+		const std::string err = g_err;
+		restore_overrides(p, o0);
+		(void)ensure_schedule(p, count);
+		g_err = err;
+	}
+	return rc;
+}
+
+} // extern "C"
+
+// The layout search of mbik_plan_autotune (plans without constraint_mode).
+static int autotune_layouts(mbik_plan *p, int first, int count, const float *pose_in, const float *targets, float *pose_out,
+		hipStream_t st) {
 	const int lanes = p->lanes_override;
 	const int staging0 = p->staging_override;
 	const int locals0 = p->locals_override;
@@ -287,6 +339,7 @@ int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const flo
 	(void)hipEventDestroy(e0);
 	(void)hipEventDestroy(e1);
 	if (rc != MBIK_OK) return rc;
+	if (timed.empty()) return kNothingTimed;
 	// Near-ties go to the earliest candidate (a fixed order), not to run-to-run timing noise
 	// (~1 %), so that boxes agree on the layout and per-layout evidence stays comparable.
 	for (const Timed &c : timed)
@@ -309,5 +362,3 @@ int32_t mbik_plan_autotune(mbik_plan *p, int32_t first, int32_t count, const flo
 	p->waves_override = best_wv;
 	return ensure_schedule(p, count);
 }
-
-} // extern "C"

@@ -124,7 +124,12 @@ int32_t mbik_multi_solve(mbik_multi *m, const float *pose_in, const float *targe
 		DeviceGuard g(m->root);
 		if (hipEventRecord(m->start, rs) != hipSuccess) return fail(MBIK_EHIP, "hipEventRecord");
 	}
+	// Shards run in order; a failing shard ends the call.  Every shard that queued anything --
+	// the failing one included -- records its done event on its stream, and the root stream waits
+	// for all of those: the scatter copies still reading the caller's pose_in / targets and the
+	// gathers writing pose_out finish before any later work on the root stream.
 	int rc = MBIK_OK;
+	size_t queued = 0;
 	for (size_t i = 0; i < m->plans.size() && rc == MBIK_OK; i++) {
 		mbik_plan *p = m->plans[i];
 		auto &s = m->sh[i];
@@ -135,31 +140,24 @@ int32_t mbik_multi_solve(mbik_multi *m, const float *pose_in, const float *targe
 			rc = fail(MBIK_EHIP, "hipStreamWaitEvent");
 			break;
 		}
+		queued = i + 1;
 		const float *in = pose_in + o * B * 10, *tg = targets ? targets + o * P * 12 : nullptr;
 		float *outp = pose_out + o * B * 10;
 		if (s.staged && n) {
 			if (hipMemcpyPeerAsync(s.in, p->device, in, m->root, n * B * 10 * sizeof(float), s.stream) != hipSuccess ||
-					(P > 0 && hipMemcpyPeerAsync(s.tg, p->device, tg, m->root, n * P * 12 * sizeof(float), s.stream) != hipSuccess)) {
+					(P > 0 && hipMemcpyPeerAsync(s.tg, p->device, tg, m->root, n * P * 12 * sizeof(float), s.stream) != hipSuccess))
 				rc = fail(MBIK_EHIP, "hipMemcpyPeerAsync (scatter)");
-				break;
-			}
-			if ((rc = mbik_solve(p, 0, (int32_t)n, s.in, s.tg, s.out, s.stream)) != MBIK_OK) break;
-			if (hipMemcpyPeerAsync(outp, m->root, s.out, p->device, n * B * 10 * sizeof(float), s.stream) != hipSuccess) {
+			else if ((rc = mbik_solve(p, 0, (int32_t)n, s.in, s.tg, s.out, s.stream)) != MBIK_OK)
+				;
+			else if (hipMemcpyPeerAsync(outp, m->root, s.out, p->device, n * B * 10 * sizeof(float), s.stream) != hipSuccess)
 				rc = fail(MBIK_EHIP, "hipMemcpyPeerAsync (gather)");
-				break;
-			}
-		} else if (n && (rc = mbik_solve(p, 0, (int32_t)n, in, tg, outp, s.stream)) != MBIK_OK) {
-			break;
+		} else if (n) {
+			rc = mbik_solve(p, 0, (int32_t)n, in, tg, outp, s.stream);
 		}
-		if (hipEventRecord(s.done, s.stream) != hipSuccess) {
-			rc = fail(MBIK_EHIP, "hipEventRecord");
-			break;
-		}
+		if (hipEventRecord(s.done, s.stream) != hipSuccess && rc == MBIK_OK) rc = fail(MBIK_EHIP, "hipEventRecord");
 	}
-	// the root stream waits for every shard that was queued (also after an error: the caller's
-	// buffers stay in use until those finish)
 	DeviceGuard g(m->root);
-	for (size_t i = 0; i < m->plans.size(); i++)
+	for (size_t i = 0; i < queued; i++)
 		if (hipStreamWaitEvent(rs, m->sh[i].done, 0) != hipSuccess && rc == MBIK_OK) rc = fail(MBIK_EHIP, "hipStreamWaitEvent");
 	return rc;
 }

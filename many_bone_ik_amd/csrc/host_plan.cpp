@@ -153,7 +153,18 @@ int blocks_per_cu(void *ctx, int64_t lds_bytes) {
 // cheap and its state lives in HBM, so the chip's VALU issue (many narrow waves), not one
 // skeleton's chain, bounds it beyond that (C2 / C3 / C5: DESIGN.md §1, profiles/r01_cmode_lanes_sweep.jsonl).
 constexpr int kCmodeLanes = 4;
-int ensure_schedule(mbik_plan *p, int64_t nlaunch) {
+// The constraint_mode wave-roles block's LDS for this launch, bounded from the host plan alone
+// (the topology blob's upper bound; cmode_lds_bytes needs the uploaded blob and node state).
+static int64_t cmode_rw_lds_bound(const mbik_plan *p, int64_t nlaunch) {
+	const mbik::HostPlan &h = p->host;
+	const int64_t W = std::max(1, (h.cm_npos + 31) / 32);
+	const int64_t spw = cmode_shape_of(p, nlaunch).spw;
+	return mbik::topology_bytes(h) + (2 * (int64_t)h.B + spw * 4 * W + (int64_t)h.K * 64 * h.cm_maxd + (int64_t)h.K * 4 * 64 + 64) * 4;
+}
+
+// roles_ok false: the classic layout even where wave roles are asked for (their block does not
+// fit the LDS, below).
+static int ensure_schedule_as(mbik_plan *p, int64_t nlaunch, bool roles_ok) {
 	mbik::HostPlan &h = p->host;
 	int lanes = p->lanes_override;
 	if (lanes == 0 && h.constraint_mode && p->cm_lanes > 0) lanes = p->cm_lanes;
@@ -162,7 +173,7 @@ int ensure_schedule(mbik_plan *p, int64_t nlaunch) {
 	h.waves_per_simd = (p->waves_override == 2 && !h.constraint_mode && h.stabilization_passes == 0) ? 2 : 1;
 	// Wave roles (mbik_plan_set_wave_roles): the whole state in device memory, one wave per role
 	// (K = 2, 4 or 8 waves per block; 8 only at two waves per SIMD), no stabilization, 32-bit tables.
-	h.wave_roles = p->roles_override == 1 && !h.constraint_mode && h.stabilization_passes == 0 && tables_fit_32(p) ? 1 : 0;
+	h.wave_roles = roles_ok && p->roles_override == 1 && !h.constraint_mode && h.stabilization_passes == 0 && tables_fit_32(p) ? 1 : 0;
 	if (h.wave_roles) {
 		const int cap = 4 * h.waves_per_simd;
 		int roles = std::min(lanes, cap);
@@ -181,7 +192,7 @@ int ensure_schedule(mbik_plan *p, int64_t nlaunch) {
 	}
 	// constraint_mode with wave roles (cmode.h mbik_cmode_kernel_rw): K = 2, 4 or 8 waves per block
 	h.cm_roles = 0;
-	if (h.constraint_mode && p->roles_override == 1 && h.stabilization_passes == 0 && tables_fit_32(p) &&
+	if (roles_ok && h.constraint_mode && p->roles_override == 1 && h.stabilization_passes == 0 && tables_fit_32(p) &&
 			node_area_floats(3 * h.B + 2 * h.NC, (size_t)h.N) * sizeof(float) < (size_t(1) << 32)) {
 		int roles = 1;
 		while (roles < (lanes > 0 ? lanes : kCmodeLanes)) roles <<= 1;
@@ -208,6 +219,14 @@ int ensure_schedule(mbik_plan *p, int64_t nlaunch) {
 	mbik::build_schedule(h, lanes, nlaunch, p->spw_override, p->interval_override, blocks_per_cu, p, p->cu_count);
 	if (lanes == 0 && h.constraint_mode && h.K > kCmodeLanes && !h.cm_roles)
 		mbik::build_schedule(h, kCmodeLanes, nlaunch, p->spw_override, p->interval_override, blocks_per_cu, p, p->cu_count);
+	// A wave-roles block holds the topology, the non-finite flags and, with cooperative rows, the
+	// block's targets and the effector-global exchange (the root segment's row alone takes a slot
+	// per pin); constraint_mode's holds per-wave chain stacks of the deepest pose chain.  Where that
+	// exceeds the LDS the plan falls back to the classic layout, as it does for stabilization or
+	// 64-bit tables: a pinned mbik_plan_set_wave_roles(1) still solves, and the autotune times the
+	// classic layout for such a candidate instead of failing on it.
+	if (roles_ok && ((h.wave_roles && h.lds_block_bytes > 160 * 1024) || (h.cm_roles && cmode_rw_lds_bound(p, nlaunch) > 160 * 1024)))
+		return ensure_schedule_as(p, nlaunch, false);
 	if (h.state_hbm == 2) {
 		// the whole state in device memory: one skeleton's LDS layout per skeleton (the locals
 		// and the checkpoint globals live in skeleton-tiled areas, d_locals and d_gtile)
@@ -270,6 +289,8 @@ int ensure_schedule(mbik_plan *p, int64_t nlaunch) {
 	p->dev.lds_stride = (mbik::lds_floats_per_skeleton(h) + 3) & ~3;
 	return MBIK_OK;
 }
+
+int ensure_schedule(mbik_plan *p, int64_t nlaunch) { return ensure_schedule_as(p, nlaunch, true); }
 
 // constraint_mode block LDS (cmode.h): topology blob, pre-order tables, the dirty words of
 // the block's 64 / K skeletons, then per lane the chain stack and, with stabilization, the

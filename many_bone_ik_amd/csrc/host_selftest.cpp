@@ -307,8 +307,8 @@ int32_t mbik_selftest_point_in_limits(const mbik_plan *p, int32_t slot, int32_t 
 	if (!p || !point || !out || !in_bounds) return fail(MBIK_EINVAL, "null argument");
 	if (slot < 0 || slot >= p->host.NC || skeleton < 0 || skeleton >= p->host.N) return fail(MBIK_EINVAL, "slot or skeleton out of range");
 	DeviceGuard guard(p->device);
-	// the topology blob the kernel reads (uploaded with the launch schedule)
-	if (int rc = ensure_schedule(const_cast<mbik_plan *>(p), p->host.N)) return rc;
+	// the topology blob the kernel reads, uploaded with the plan's launch schedule (finish_plan):
+	// the plan is only read here, never rescheduled, so a solve of it may be in flight
 	if (!p->dev.topo_blob) return fail(MBIK_EHIP, "plan has no topology blob");
 	DevBuf o, ib;
 	int rc = o.put(nullptr, 6 * sizeof(float));

@@ -11,7 +11,7 @@ import pytest
 from many_bone_ik_amd import workloads as W
 from many_bone_ik_amd.solver import Plan
 
-from .test_gpu_constraint_mode import run_frames
+from .test_gpu_constraint_mode import animate, run_frames
 from .test_gpu_edge_cases import CASES
 from .test_gpu_fuzz import random_case
 from .test_gpu_parity import assert_parity, torch_dev  # noqa: F401 (fixture)
@@ -119,3 +119,31 @@ def test_save_load_keeps_wave_roles(oracle, mbik):
     assert_parity(got, ref_o.solve(pose, wl.targets), "frame 1 after load")
     assert plan2.info()["wave_roles"] == 1
     plan2.close()
+
+
+def test_c5_full_size_two_frames(oracle, mbik):
+    """The constraint_mode bench line's layout at its timed size: C5, 16,384
+    skeletons on the wave-roles kernel with K = 8 waves and 64 skeletons per block, two frames (the
+    second from the first's output, animated).  The node caches of every skeleton advance on the
+    GPU; oracle object graphs of the skeletons at the start, the middle and the end of the batch
+    take the same inputs and must give the same bits each frame."""
+    n = 16384
+    wl = W.generate(5, n)
+    plan = Plan.from_workload(wl, constraint_mode=True, lanes=8)
+    plan.set_wave_roles(1)
+    windows = [(0, 3), (n // 2 - 1, 3), (n - 4, 4)]
+    graphs = [oracle.Oracle(W.generate(5, k, first=f), constraint_mode=True) for f, k in windows]
+    rng = np.random.default_rng(91)
+    pose = wl.pose
+    for frame in range(2):
+        got = plan.solve_host(pose, wl.targets)
+        info = plan.info()
+        assert info["wave_roles"] == 1 and info["lanes_per_skeleton"] == 8 and info["skeletons_per_block"] == 64, info
+        assert np.isfinite(got).all()
+        for (f, k), o in zip(windows, graphs):
+            ref = o.solve(np.ascontiguousarray(pose[f:f + k]), np.ascontiguousarray(wl.targets[f:f + k]), threads=4)
+            assert_parity(got[f:f + k], ref, f"C5 constraint_mode K8 frame {frame} @{f}")
+        pose = animate(got, rng)
+    plan.close()
+    for o in graphs:
+        o.close()

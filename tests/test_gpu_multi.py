@@ -71,3 +71,27 @@ def test_multi_argument_checks(mbik):
     assert m.skeletons() == (16, [0, 8, 16])
     with pytest.raises(_lib.MbikError):
         m.solve(0, 0, 0)
+
+
+def test_bench_library_multi_on_one_box(mbik, torch_dev):
+    """bench.py's library_multi measurement: at N > 1 rank 0 times
+    mbik_multi_solve over one plan per visible device while the other ranks wait.  The same
+    code on the one-GPU box, with both plans on device 0, run as the driver runs bench.py:
+    the line carries the measurement and its oracle checks at both ends of the batch."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--config", "2", "--skeletons", "256", "--steps", "2",
+           "--warmup", "1", "--no-cpu-baseline", "--no-autotune", "--library-multi-devices", "0,0"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    lm = line["library_multi"]
+    assert "error" not in lm, lm
+    assert lm["devices"] == [0, 0] and lm["plans"] == 2 and lm["skeletons"] == 256 and lm["ms_per_frame"] > 0
+    assert [c["range"] for c in lm["parity"]] == [[0, 16], [240, 256]]
+    assert all(c["bitwise_equal"] for c in lm["parity"]), lm["parity"]
+    # the line's own parity check covers both ends of the rank's batch as well
+    assert line["parity"]["ranges"] == [[0, 32], [224, 256]] and line["parity"]["bitwise_equal"]

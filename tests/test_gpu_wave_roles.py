@@ -167,10 +167,12 @@ def test_wave_roles_save_load(oracle, mbik):
     assert np.array_equal(got.view(np.uint32), first.view(np.uint32))
 
 
-@pytest.mark.parametrize("cfg,n,k", [(4, 32768, 4), (5, 16384, 8)])
+@pytest.mark.parametrize("cfg,n,k", [(4, 32768, 4), (5, 16384, 8), (4, 262144, 4)])
 def test_wave_roles_full_size(oracle, mbik, torch_dev, cfg, n, k):
-    """BASELINE sizes on the layouts the bench times: whole-batch properties and oracle spot
-    checks at both ends and inside."""
+    """BASELINE sizes on the layouts the bench times (K4 / K8 at two waves per SIMD; C4's whole
+    262,144-skeleton batch is the strong-scaling line's layout, where the device-memory state
+    areas and their 32-bit buffer offsets are largest): whole-batch properties and oracle checks
+    at the start, a third in, the middle and the last six skeletons."""
     torch, dev = torch_dev
     wl = W.generate(cfg, n)
     plan = rw_plan(wl, k, 2)
@@ -179,14 +181,16 @@ def test_wave_roles_full_size(oracle, mbik, torch_dev, cfg, n, k):
     po = torch.empty_like(pi)
     plan.solve(pi.data_ptr(), tg.data_ptr(), po.data_ptr(), 0, wl.n, torch.cuda.current_stream(dev).cuda_stream)
     torch.cuda.synchronize()
+    check_info(plan, k, 2)
     got = po.cpu().numpy()
+    del pi, tg, po
     assert np.isfinite(got).all()
     q = got[..., :4]
     assert np.abs(np.linalg.norm(q, axis=-1) - 1).max() < 1e-5
-    for first in (0, 4093, n // 2 + 17, n - 3):
-        sub = W.generate(cfg, 3, first=first)
+    for first, cnt in ((0, 3), (4093, 3), (n // 3, 3), (n // 2 + 17, 3), (n - 6, 6)):
+        sub = W.generate(cfg, cnt, first=first)
         ref = oracle.Oracle(sub).solve(sub.pose, sub.targets, threads=8)
-        assert_parity(got[first:first + 3], ref, f"C{cfg} wave roles full size @{first}")
+        assert_parity(got[first:first + cnt], ref, f"C{cfg} wave roles full size @{first}")
 
 
 def test_wave_roles_plan_in_a_group(oracle, mbik, torch_dev):
