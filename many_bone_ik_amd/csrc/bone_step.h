@@ -179,6 +179,75 @@ __device__ __forceinline__ void help_part_b(const DevPlan &t, int k, const X3 &P
 	hw_store(rec, f, 6, kHelpF4);
 }
 
+// ---- Wave roles, cooperative segments: the parent-side record of the group's second wave ----
+// While a cooperative group's first wave runs bone-step k's chain, the group's other waves wait
+// at the block barrier.  The second wave instead computes step k + 1's parent-side values --
+// they depend only on iteration-start state, as the helper wave's records do (a tip -> root pass
+// leaves the ancestors unsolved): the parent's global P, the bone's origin Gb.o, inverse(P.b),
+// xform(inverse(P.b), -P.o) and the slerp's p_to side -- with bone_step's own operations on the
+// same inputs, so the first wave reads the bits it would have computed.  Layout as the helper
+// ring's, [float4 field][64 lanes], one record per group (kernels.h kRwRecF4; the writes of step
+// k + 1's record come after the barrier that ends step k, when its reader is done).
+enum RwRecField { RF_P = 0, RF_GBO = 12, RF_PINV = 15, RF_PNP = 24, RF_STO = 27 };
+struct RwRec {
+	X3 P;
+	V3 gbo;
+	B3 Pinv;
+	V3 pnp;
+	SlerpTo sto;
+};
+template <class LV, class GV>
+__device__ __forceinline__ RwRec rw_record(const DevPlan &t, int k, const LV &L, const GV &G) {
+	const int4 sr = t.step_rec[k];
+	const int b = sr.x & 0xffff;
+	const int flags = sr.z & 0xffff;
+	RwRec r;
+	r.P = xid();
+	if (flags & mbik::SR_PARENT_GLOBAL) {
+		r.P = G.ld((sr.y & 0xffff) - 1);
+		for (int q = (sr.x >> 16) - 2; q > k; q--) r.P = r.P * L.ld(t.seg_bones[q]);
+	}
+	r.Pinv = inverse(r.P.b);
+	const X3 Lb = L.ld(b);
+	const X3 Gb = (flags & mbik::SR_HAS_POSE_PARENT) ? r.P * Lb : Lb;
+	r.gbo = Gb.o;
+	r.pnp = xform(r.Pinv, -r.P.o);
+	r.sto = slerp_to(Gb.b);
+	return r;
+}
+// The second wave's wait until the group's first wave has read the current record (its counter
+// reaches v).  Every wait has an exit, as the helper wave's: when the counter has not moved for
+// `timeout` wall-clock ticks (help_expired) the wave raises the block's gave-up word and stops
+// waiting for the rest of the launch; the block then writes its skeletons as failures
+// (write_help_timeout) and sets the plan's timeout flag, as a helper-wave block does.
+__device__ __forceinline__ void rw_wait(const int *cnt, int v, bool &stuck, int *gave_up, uint64_t timeout) {
+	if (stuck) return;
+	uint64_t t0 = 0, tl = 0;
+	int seen = 0;
+	for (;;) {
+		const int c = __builtin_amdgcn_readfirstlane(__hip_atomic_load(cnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+		if (c >= v) return;
+		if (help_expired(t0, tl, seen, c, timeout)) {
+			stuck = true;
+			__hip_atomic_store(gave_up, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+			return;
+		}
+		__builtin_amdgcn_s_sleep(1);
+	}
+}
+__device__ __forceinline__ void rw_record_store(float4 *rec, const RwRec &r) {
+	float f[4 * mbik::kRwRecF4];
+	hw_b(f, RF_P, r.P.b);
+	hw_v(f, RF_P + 9, r.P.o);
+	hw_v(f, RF_GBO, r.gbo);
+	hw_b(f, RF_PINV, r.Pinv);
+	hw_v(f, RF_PNP, r.pnp);
+	f[RF_STO] = r.sto.q.x; f[RF_STO + 1] = r.sto.q.y; f[RF_STO + 2] = r.sto.q.z; f[RF_STO + 3] = r.sto.q.w;
+	f[RF_STO + 4] = r.sto.len[0]; f[RF_STO + 5] = r.sto.len[1]; f[RF_STO + 6] = r.sto.len[2];
+	for (int i = RF_STO + 7; i < 4 * mbik::kRwRecF4; i++) f[i] = 0.0f;
+	hw_store(rec, f, 0, mbik::kRwRecF4);
+}
+
 // Staged-heading record (multi-lane segments): the 11 QCP::inner_product terms of one heading
 // pair, as floats -- wc1_a * c2_b (a, b = x, y, z), dot(wc1, c1), dot(c2, c2).
 constexpr int HS_REC = 12;
@@ -227,7 +296,9 @@ __device__ __forceinline__ void qcp_accumulate(QSums &S, const V3 wc1, const V3 
 // 5): only the two-waves-per-SIMD build, so that the one-wave kernels keep their registers.
 // SEL: the orthonormalizations' zero-vector tests as selects (normalized_sel; the one-wave builds).
 // XW (wave roles): xs marks a cooperative segment whose effector globals the group's waves left in
-// the exchange area xw (coop_walk); this wave, the group's first, consumes them.
+// the exchange area xw (coop_walk); this wave, the group's first, consumes them, and with hrec
+// its parent-side values come from the group's second wave's record (rw_record): it reads the
+// whole record first and posts hseq in the group's counter hfl (rw_wait).
 template <bool STAB, bool PR, int TA, bool HELP, bool XS, int PM, bool SEL, bool XW, class LV, class GV, class FP, class IP>
 __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, int xs, size_t s, const LV &L, const GV &G, const FP TG,
 		const FP ST, const IP SF, const FP HS, const FP OE, const FP MS, double &prev_dev, const EffPre &pre, bool hoist,
@@ -248,8 +319,24 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, int xs
 	// from the nearest checkpoint above it, with the global pass's own products.
 	X3 P = xid();
 	B3 Pinv;
+	// wave roles: a cooperative segment's step with its parent-side record (rw_record)
+	const bool rrec = XW && xs && hrec != nullptr;
+	V3 rgbo, rpnp;
+	SlerpTo rsto;
 	if constexpr (HELP) {
 		// (P, Pinv: read after the wait for the record's part B, below)
+	} else if (rrec) {
+		P = hrx(hrec, RF_P);
+		Pinv = hrb(hrec, RF_PINV);
+		rgbo = hrv(hrec, RF_GBO);
+		rpnp = hrv(hrec, RF_PNP);
+		rsto.q = q4(hrf(hrec, RF_STO), hrf(hrec, RF_STO + 1), hrf(hrec, RF_STO + 2), hrf(hrec, RF_STO + 3));
+		rsto.len[0] = hrf(hrec, RF_STO + 4);
+		rsto.len[1] = hrf(hrec, RF_STO + 5);
+		rsto.len[2] = hrf(hrec, RF_STO + 6);
+		// read: the group's second wave may store the next step's record (test hook: a first wave
+		// that stops posting after record help_drop, mbik_plan_debug_helper)
+		if (t.help_drop < 0 || hseq <= t.help_drop) help_post(hfl, hseq);
 	} else {
 		if (flags & mbik::SR_PARENT_GLOBAL) {
 			P = G.ld((sr.y & 0xffff) - 1);
@@ -266,6 +353,10 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, int xs
 	SlerpTo sto;
 	if constexpr (HELP) {
 		Gb = hrx(hrec, HF_GB);
+	} else if (rrec) {
+		// (a cooperative segment has two or more effectors: its headings read only Gb.o)
+		Gb = X3{B3{}, rgbo};
+		sto = rsto;
 	} else {
 		Gb = hasP ? P * Lb : Lb;
 		sto = slerp_to(Gb.b);
@@ -721,7 +812,7 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, int xs
 	X3 result = {Gn.b, Gn.o + translation};
 	// affine_inverse(P) with P.basis.inverse() already at hand (same arithmetic)
 	if constexpr (HELP) Lb = hasP ? X3{Pinv, hrv(hrec, HF_PNP)} * result : result;
-	else Lb = hasP ? X3{Pinv, xform(Pinv, -P.o)} * result : result;
+	else Lb = hasP ? X3{Pinv, rrec ? rpnp : xform(Pinv, -P.o)} * result : result;
 	// set_global_pose propagates through b's subtree: pinned children's stale
 	// bone-direction caches are refreshed from here on.
 	// Every lane of the group holds identical values, so each writes its own copy (same

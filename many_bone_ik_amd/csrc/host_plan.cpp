@@ -66,6 +66,14 @@ int upload_topology(mbik_plan *p) {
 		return fail(MBIK_EHIP, "hipMemcpy topology blob");
 	d.topo_blob = reinterpret_cast<const uint4 *>(p->d_sched);
 	d.topo_words = (int)blob.size();
+	// diagnostics (tools/topo_const.py): the blob's table offsets, for a timing-only build that
+	// compiles one plan's offsets in (solve_block.h MBIK_TOPO_CONST)
+	if (getenv("MBIK_DEBUG_TOPO_OFFSETS")) {
+#define MBIK_PRINT(T, name) fprintf(stderr, "MBIK_TC %s %d\n", #name, d.o_##name);
+		MBIK_TOPO_TABLES(MBIK_PRINT)
+#undef MBIK_PRINT
+		fprintf(stderr, "MBIK_TC_K %d\n", h.K);
+	}
 	return MBIK_OK;
 }
 
@@ -513,9 +521,13 @@ int launch(mbik_plan *p, int first, int count, const float *pose_in, const float
 	unsigned threads = 64;
 	if (h.wave_roles) {
 		threads = 64u * (unsigned)h.K; // a wave per role
-		// non-finite flags; with cooperative rows the targets and the effector-global exchange
-		lds += 64 * sizeof(int) + (h.rw_xslots ? ((size_t)h.P + h.rw_xslots) * 12 * 64 * sizeof(float) : 0);
+		// non-finite flags; with cooperative rows the targets, the effector-global exchange and the
+		// groups' parent-side records
+		lds += 64 * sizeof(int) + (h.rw_xslots ? ((size_t)h.P + h.rw_xslots) * 12 * 64 * sizeof(float) + mbik::rw_record_bytes(h) : 0);
 		if (lds > 160 * 1024) return fail(MBIK_EUNSUPPORTED, "wave roles: a row's effector-global exchange exceeds the LDS");
+		// the cooperative groups' record handshake has a deadline and reports through the plan's
+		// timeout flag, as the helper wave's does (rw_wait)
+		if (h.rw_xslots && (rc = ensure_help_flag(p)) != MBIK_OK) return rc;
 	} else if (helper_on(p)) {
 		if ((rc = ensure_help_flag(p)) != MBIK_OK) return rc;
 		lds += kHelpRingBytes;

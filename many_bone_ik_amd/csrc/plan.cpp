@@ -912,7 +912,12 @@ void build_schedule(HostPlan &p, int32_t lanes, int64_t nlaunch, int32_t spw_ove
 	}
 	p.spw = best;
 	p.lds_block_bytes = best * (int64_t)(((lds_floats_per_skeleton(p) + 3) & ~3) * 4) + topo +
-			(p.wave_roles ? 64 * 4 + (p.rw_xslots ? ((int64_t)p.P + p.rw_xslots) * 12 * 64 * 4 : 0) : 0);
+			(p.wave_roles ? 64 * 4 + (p.rw_xslots ? ((int64_t)p.P + p.rw_xslots) * 12 * 64 * 4 + rw_record_bytes(p) : 0) : 0);
+}
+
+int64_t rw_record_bytes(const HostPlan &p) {
+	// K / 2 records, then K / 2 counters and the block's gave-up word (16-byte aligned)
+	return p.wave_roles && p.rw_xslots ? (int64_t)(p.K / 2) * kRwRecF4 * 64 * 16 + ((p.K / 2 + 1) * 4 + 15) / 16 * 16 : 0;
 }
 
 } // namespace mbik

@@ -210,5 +210,10 @@ void build_schedule(HostPlan &plan, int32_t lanes_per_skeleton, int64_t skeleton
 int32_t lds_floats_per_skeleton(const HostPlan &plan);
 int32_t state_floats_per_skeleton(const HostPlan &plan);
 int64_t topology_bytes(const HostPlan &plan);
+// Wave roles: the parent-side record of a cooperative group (bone_step.h rw_record), kRwRecF4
+// float4 per lane, one per group of a row (at most K / 2 groups of two or more waves), and the
+// groups' counters (rw_wait), after the effector-global exchange; 0 without cooperative rows.
+constexpr int kRwRecF4 = 9;
+int64_t rw_record_bytes(const HostPlan &plan);
 
 } // namespace mbik

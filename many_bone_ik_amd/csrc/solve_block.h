@@ -50,7 +50,14 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 	// ordered before its reads already
 	if constexpr (HELP || RW > 1) __syncthreads();
 	const uint32_t *topo = reinterpret_cast<const uint32_t *>(lds4);
+#ifdef MBIK_TOPO_CONST
+	// timing-only diagnostic build (tools/topo_const.py): one plan's table offsets compiled in, so
+	// that no SGPR holds them; any other plan reads wrong tables
+#include "topo_const.h"
+#define MBIK_REPOINT(T, name) t.name = reinterpret_cast<const T *>(topo + MBIK_TC_##name);
+#else
 #define MBIK_REPOINT(T, name) t.name = reinterpret_cast<const T *>(topo + t.o_##name);
+#endif
 	MBIK_TOPO_TABLES(MBIK_REPOINT)
 #undef MBIK_REPOINT
 	float *lds = reinterpret_cast<float *>(lds4) + t.topo_words;
@@ -111,8 +118,14 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 	// the exchange area: the cooperative consumer reads them for every effector at every step)
 	float *xt = RW ? lds + 64 : nullptr;
 	float *xw = RW ? xt + (t.rw_xslots ? (size_t)t.P * (12 * 64) : 0) : nullptr;
+	// (then the cooperative groups' parent-side records, kRwRecF4 float4 x 64 lanes each, K / 2 of
+	// them: rw_record; then one counter per group and the block's gave-up word: rw_wait)
+	float4 *xr4 = RW ? reinterpret_cast<float4 *>(xw + (size_t)t.rw_xslots * (12 * 64)) : nullptr;
+	int *rw_cnt = RW ? reinterpret_cast<int *>(xr4 + (K / 2) * (mbik::kRwRecF4 * 64)) : nullptr;
+	bool rw_stuck = false; // this wave gave up waiting for its group's first wave (rw_wait)
 	if constexpr (RW) {
 		if (threadIdx.x < 64) nf_rw[threadIdx.x] = 0;
+		if (t.rw_xslots && threadIdx.x <= K / 2) rw_cnt[threadIdx.x] = 0; // counters, gave-up word
 	}
 	if (valid && (RW || wave == 0)) {
 		for (int b = role; b < B; b += K)
@@ -260,7 +273,11 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 					// effectors' paths (coop_walk) and meet; each group's first wave -- and each wave
 					// of a segment solved alone -- runs the step; the block meets again before the
 					// next step walks from the bones just solved.  Every wave runs the row's step
-					// count, so the barriers match.
+					// count, so the barriers match.  Meanwhile a group's second wave computes the next
+					// step's parent-side record (rw_record): the first wave reads its record at the
+					// start of its step and posts that in the group's LDS counter, and the second wave
+					// stores the next record once the counter shows it (rw_wait; the first step's
+					// record is stored before the row's first walk).
 					const int4 task = t.sched[r * K + role];
 					const bool act = valid && task.x >= seg_lo && task.x <= seg_hi;
 					const int seg = task.x >= 0 ? task.x : 0;
@@ -272,6 +289,18 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 					const int e0 = t.seg_eff_off[seg];
 					const bool hoist = HOIST && act && !coop && t.seg_eff_off[seg + 1] - e0 == 1;
 					if (hoist) load_eff<TA>(t, t.seg_effs[e0], TG, s, t.seg_hw + t.seg_hw_off[seg] + t.seg_eff_hoff[e0], pre);
+					// the group's record and counter: the groups of a row have equal sizes, so the
+					// group is its first wave's index / m (the wave's task is uniform: readfirstlane
+					// makes the role branches scalar)
+					const int ty = __builtin_amdgcn_readfirstlane(task.y);
+					const bool rec_on = coop;
+					const int grp = rec_on ? (role - ty) / __builtin_amdgcn_readfirstlane(task.z) : 0;
+					float4 *rec = rec_on ? xr4 + grp * (mbik::kRwRecF4 * 64) + lane : nullptr;
+					int *rcnt = rec_on ? rw_cnt + grp : nullptr;
+					const bool leader = ty == 0;
+					const bool producer = rec_on && ty == 1;
+					if (leader && rec_on) *rcnt = 0; // (read only after the row's first barrier)
+					if (producer && act && k0 < k1) rw_record_store(rec, rw_record(t, k0, L, G));
 					// (MBIK_PROF, wave roles: 18 packed / plain rows, 19 coop_walk, 21 waiting at the
 					// cooperative rows' barriers, 22 the steps run after them, 23 cooperative rows)
 					MBIK_PROF_T(cr0);
@@ -284,9 +313,16 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 						__syncthreads();
 						MBIK_PROF_T(c2);
 						MBIK_PROF_ADD(21, c1, c2);
-						if (step && task.y == 0)
-							bone_step<false, true, TA, false, false, PM, HOIST, true>(t, seg, k0 + q, 0, 1, coop ? 1 : 0, s, L, G, TG, ST, SF,
-									HS, OE, MS, prev_dev, pre, hoist, nullptr, nullptr, 0, nullptr, xw MBIK_PROF_ARG);
+						if (leader) {
+							if (step)
+								bone_step<false, true, TA, false, false, PM, HOIST, true>(t, seg, k0 + q, 0, 1, coop ? 1 : 0, s, L, G, TG, ST,
+										SF, HS, OE, MS, prev_dev, pre, hoist, rec, rcnt, q + 1, nullptr, xw MBIK_PROF_ARG);
+						} else if (producer && act && k0 + q + 1 < k1) {
+							// the next step's record, stored once the first wave has read this step's
+							const RwRec next = rw_record(t, k0 + q + 1, L, G);
+							rw_wait(rcnt, q + 1, rw_stuck, rw_cnt + K / 2, t.help_timeout);
+							rw_record_store(rec, next);
+						}
 						MBIK_PROF_T(c3);
 						MBIK_PROF_ADD(22, c2, c3);
 						__syncthreads();
@@ -336,6 +372,11 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 			MBIK_PROF_ADD(18, pr0, pr1);
 			r = r1;
 		}
+	}
+	if constexpr (RW) {
+		// a wave that gave up in rw_wait raised the block's word before the row's last barrier
+		if (t.rw_xslots)
+			help_stuck = __builtin_amdgcn_readfirstlane(__hip_atomic_load(rw_cnt + K / 2, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) != 0;
 	}
 	MBIK_PROF_T(pk2);
 	bool bad = false;

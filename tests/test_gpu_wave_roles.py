@@ -223,3 +223,37 @@ def test_wave_roles_partly_filled_waves(oracle, mbik, cfg, n, k, spw):
     info = plan.info()
     assert info["wave_roles"] == 1 and info["skeletons_per_block"] == spw
     assert_parity(got, ref, f"C{cfg} wave roles K={k} spw={spw}")
+
+
+@pytest.mark.parametrize("cfg,k", [(4, 4), (5, 8)])
+def test_wave_roles_record_handshake_has_an_exit(oracle, mbik, torch_dev, cfg, k):
+    """A cooperative group's parent-side records (bone_step.h rw_record / rw_wait): the group's
+    first wave posts each record it has read, and the second wave stores the next one only then.
+    Test hook (mbik_plan_debug_helper): the first wave stops posting after record 1, with a 20 ms
+    deadline.  The second wave gives up instead of hanging; every skeleton of the launch is written
+    as a failure and flagged, the plan's status and next call report the timeout, and with the hook
+    off the plan is exact again."""
+    from many_bone_ik_amd import _lib
+    from .test_gpu_helper_wave import _timeout_marker_ok
+    torch, dev = torch_dev
+    wl = W.generate(cfg, 70, first=60500 + cfg)
+    ref = oracle.Oracle(wl).solve(wl.pose, wl.targets, threads=8)
+    plan = rw_plan(wl, k, 2)
+    plan.debug_helper(1, 20000)
+    pi = torch.from_numpy(wl.pose).to(dev)
+    tg = torch.from_numpy(wl.targets).to(dev)
+    po = torch.empty_like(pi)
+    flags = torch.zeros(wl.n, dtype=torch.uint8, device=dev)
+    plan.solve_checked(pi.data_ptr(), tg.data_ptr(), po.data_ptr(), flags.data_ptr())
+    torch.cuda.synchronize()
+    assert plan.status() == 1
+    assert flags.cpu().numpy().all()
+    assert _timeout_marker_ok(po.cpu().numpy())
+    with pytest.raises(_lib.MbikError) as e:
+        plan.solve(pi.data_ptr(), tg.data_ptr(), po.data_ptr())
+    assert e.value.code == _lib.MBIK_EHIP
+    plan.debug_helper(-1, 0)
+    plan.solve(pi.data_ptr(), tg.data_ptr(), po.data_ptr())
+    torch.cuda.synchronize()
+    assert plan.status() == 0
+    assert_parity(po.cpu().numpy(), ref, f"C{cfg} wave roles after the handshake timeout")
