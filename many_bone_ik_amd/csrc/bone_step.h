@@ -21,6 +21,26 @@ __device__ __forceinline__ void wave_sync_lds() {
 	__builtin_amdgcn_wave_barrier();
 	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+// The parent's iteration-start global of bone-step k (step record sr): its checkpoint, times the
+// locals of the bones between that checkpoint and the step's bone (none when no checkpoint is
+// skipped), with the global pass's own products in its order.  The first three of those locals
+// load together before the products (sparse checkpoints with the locals in device memory: C3's
+// interval-4 layout waited for each load in turn; same products, same order).
+template <class LV, class GV>
+__device__ __forceinline__ X3 parent_global(const DevPlan &t, const int4 sr, int k, const LV &L, const GV &G) {
+	X3 P = G.ld((sr.y & 0xffff) - 1);
+	const int q0 = (sr.x >> 16) - 2;
+	if (q0 > k) {
+		const X3 a = L.ld(t.seg_bones[q0]);
+		const X3 b = L.ld(t.seg_bones[max(q0 - 1, k + 1)]);
+		const X3 c = L.ld(t.seg_bones[max(q0 - 2, k + 1)]);
+		P = P * a;
+		if (q0 - 1 > k) P = P * b;
+		if (q0 - 2 > k) P = P * c;
+		for (int q = q0 - 3; q > k; q--) P = P * L.ld(t.seg_bones[q]);
+	}
+	return P;
+}
 // ---- Helper wave (HELP, fully resident placement-0 launches) ----
 // A bone-step's parent-side work depends only on the iteration-start state: the parent's global
 // P (a checkpoint, or rebuilt from one through ancestors not yet solved this iteration), the
@@ -144,8 +164,7 @@ __device__ __forceinline__ void help_part_a(const DevPlan &t, int k, const LV &L
 	const bool hasP = (flags & mbik::SR_HAS_POSE_PARENT) != 0;
 	P = xid();
 	if (flags & mbik::SR_PARENT_GLOBAL) {
-		P = G.ld((sr.y & 0xffff) - 1);
-		for (int q = (sr.x >> 16) - 2; q > k; q--) P = P * L.ld(t.seg_bones[q]);
+		P = parent_global(t, sr, k, L, G);
 	}
 	const X3 Lb = L.ld(b);
 	const X3 Gb = hasP ? P * Lb : Lb;
@@ -204,8 +223,7 @@ __device__ __forceinline__ RwRec rw_record(const DevPlan &t, int k, const LV &L,
 	RwRec r;
 	r.P = xid();
 	if (flags & mbik::SR_PARENT_GLOBAL) {
-		r.P = G.ld((sr.y & 0xffff) - 1);
-		for (int q = (sr.x >> 16) - 2; q > k; q--) r.P = r.P * L.ld(t.seg_bones[q]);
+		r.P = parent_global(t, sr, k, L, G);
 	}
 	r.Pinv = inverse(r.P.b);
 	const X3 Lb = L.ld(b);
@@ -339,8 +357,7 @@ __device__ void bone_step(const DevPlan &t, int seg, int k, int j, int m, int xs
 		if (t.help_drop < 0 || hseq <= t.help_drop) help_post(hfl, hseq);
 	} else {
 		if (flags & mbik::SR_PARENT_GLOBAL) {
-			P = G.ld((sr.y & 0xffff) - 1);
-			for (int q = (sr.x >> 16) - 2; q > k; q--) P = P * L.ld(t.seg_bones[q]); // none when no checkpoint is skipped
+			P = parent_global(t, sr, k, L, G);
 		}
 		Pinv = inverse(P.b);
 	}
@@ -1057,8 +1074,7 @@ __device__ void coop_walk(const DevPlan &t, int seg, int k, int j, int m, size_t
 	const int d0 = sr.z >> 16;
 	X3 P = xid();
 	if (flags & mbik::SR_PARENT_GLOBAL) {
-		P = G.ld((sr.y & 0xffff) - 1);
-		for (int q = (sr.x >> 16) - 2; q > k; q--) P = P * L.ld(t.seg_bones[q]);
+		P = parent_global(t, sr, k, L, G);
 	}
 	const X3 Lb = L.ld(b);
 	const X3 Gb = (flags & mbik::SR_HAS_POSE_PARENT) ? P * Lb : Lb;
@@ -1075,7 +1091,7 @@ __device__ void coop_walk(const DevPlan &t, int seg, int k, int j, int m, size_t
 		const int lc[2] = {i > i0 ? t.seg_eff_lcp[i] : 0, i + 1 < i1 ? t.seg_eff_lcp[i + 1] : 0};
 		X3 E;
 		Headings H; // (unused: the group's first wave builds the headings from E)
-		effector_headings<TA, PM>(t, t.seg_effs[i], d0, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, TG, 0, &pc, lc, &E);
+		effector_headings<TA, PM, true>(t, t.seg_effs[i], d0, Gb, L, TG, ST, SF, s, hw + t.seg_eff_hoff[i], H, TG, 0, &pc, lc, &E);
 		float *r = xe + (size_t)(i - e0) * (12 * 64);
 		r[0] = E.b.r[0].x; r[64] = E.b.r[0].y; r[128] = E.b.r[0].z;
 		r[192] = E.b.r[1].x; r[256] = E.b.r[1].y; r[320] = E.b.r[1].z;

@@ -52,6 +52,11 @@ using mbik::kLocTile;
 using mbik::kRowTile;
 using mbik::kPrioDefault;
 
+#ifndef MBIK_DEEP_WALK
+#define MBIK_DEEP_WALK 4
+#endif
+constexpr int kDeepWalk = MBIK_DEEP_WALK; // path bones in flight in a cooperative walk (effector_headings DEEP)
+
 // ------------------------------------------------------------------------------------
 // small device helpers
 // ------------------------------------------------------------------------------------
@@ -513,7 +518,9 @@ struct PathCk {
 	X3 x;
 	int d;
 };
-template <int PM, class LV, class FP, class IP>
+// DEEP: the wave-roles cooperative walks (coop_walk): kDeepWalk path bones in flight when the
+// locals are in device memory (outside bone_step, whose register peak they would raise).
+template <int PM, bool DEEP = false, class LV, class FP, class IP>
 __device__ __forceinline__ void effector_headings(const DevPlan &t, const EffPre &p, int d0, const X3 &Gb, const LV &L,
 		const FP ST, const IP SF, Headings &H, const FP OE, int oe_mode = 0, PathCk *pc = nullptr, const int *lcp = nullptr,
 		X3 *eout = nullptr) {
@@ -532,6 +539,27 @@ __device__ __forceinline__ void effector_headings(const DevPlan &t, const EffPre
 		// loop's instructions were those moves); the last trip's look-ahead re-reads path[b].
 		auto walk = [&](int a, int b) {
 			if (a > b) return;
+			// locals in device memory, cooperative walks: kDeepWalk path bones in flight, a rotating
+			// set of loads, each refill reading the bone kDeepWalk products ahead (clamped to b);
+			// the products are the same, in the same order
+			if constexpr (DEEP && !std::is_same_v<LV, LocContig>) {
+				constexpr int A = kDeepWalk;
+				X3 Lq[A];
+#pragma unroll
+				for (int u = 0; u < A; u++) Lq[u] = L.ld_walk(t.eff_path[off + min(a + u, b)]);
+				int d = a;
+				for (; d + A - 1 <= b; d += A) {
+#pragma unroll
+					for (int u = 0; u < A; u++) {
+						X = X * Lq[u];
+						Lq[u] = L.ld_walk(t.eff_path[off + min(d + u + A, b)]);
+					}
+				}
+#pragma unroll
+				for (int u = 0; u < A - 1; u++)
+					if (d + u <= b) X = X * Lq[u];
+				return;
+			}
 			X3 L0 = L.ld_walk(t.eff_path[off + a]);
 			int d = a;
 			// locals in LDS (placement 0): the first trip peeled out of the loop (C2 -1.1 %; the
@@ -590,13 +618,13 @@ __device__ __forceinline__ void effector_headings(const DevPlan &t, const EffPre
 	}
 	heading_terms<PM>(p, E, oe, Gb.o, H);
 }
-template <int TA, int PM, class LV, class FP, class IP>
+template <int TA, int PM, bool DEEP = false, class LV, class FP, class IP>
 __device__ __forceinline__ void effector_headings(const DevPlan &t, int e, int d0, const X3 &Gb, const LV &L,
 		const FP TG, const FP ST, const IP SF, size_t s, const double *hw, Headings &H, const FP OE,
 		int oe_mode = 0, PathCk *pc = nullptr, const int *lcp = nullptr, X3 *eout = nullptr) {
 	EffPre p;
 	load_eff<TA, PM>(t, e, TG, s, hw, p);
-	effector_headings<PM>(t, p, d0, Gb, L, ST, SF, H, OE, oe_mode, pc, lcp, eout);
+	effector_headings<PM, DEEP>(t, p, d0, Gb, L, ST, SF, H, OE, oe_mode, pc, lcp, eout);
 }
 
 // The heading pairs of effector p.e (ik_effector_3d.cpp:90-149): E = the effector bone's
