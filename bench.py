@@ -69,6 +69,9 @@ def parse():
     ap.add_argument("--stabilization-passes", type=int, default=0)
     ap.add_argument("--library-multi-devices", default="",
                     help="comma-separated devices for the library_multi measurement (default at N > 1: 0..N-1)")
+    ap.add_argument("--pmc", choices=["auto", "on", "off", "child"], default=os.environ.get("MBIK_BENCH_PMC", "auto"),
+                    help="measure roofline.traffic and the VALU issue of the timed layout in this run with rocprofv3 "
+                         "--pmc children (auto: at N=1 when rocprofv3 is present and this run is not itself profiled)")
     ap.add_argument("--traffic-json", default=os.path.join(HERE, "profiles", "traffic.json"))
     ap.add_argument("--valu-mix-json", default=os.path.join(HERE, "profiles", "valu_mix.json"))
     return ap.parse_args()
@@ -231,7 +234,7 @@ def main():
 
     # PCIe-inclusive rate (host buffers in, solve, host buffers out): reported, never `value`
     pcie = None
-    if rank == 0:
+    if rank == 0 and args.pmc != "child":
         plan.solve_host(wl.pose, wl.targets)
         reps = 5
         h0 = time.perf_counter()
@@ -244,7 +247,7 @@ def main():
     # parity spot check against the oracle (not timed): this rank's first 32 and last 32
     # skeletons, so the largest per-skeleton offsets of the timed launch are checked too
     parity = None
-    if not args.no_parity and rank == 0:
+    if not args.no_parity and rank == 0 and args.pmc != "child":
         try:
             from oracle import pyoracle as po
             head = min(32, n)
@@ -301,11 +304,17 @@ def main():
         (f"_stab{args.stabilization_passes}" if args.stabilization_passes else "")
     # the PMC traffic of exactly the layout timed here (autotune may pick differently per box)
     tkey = key + "_" + layout_key(info)
-    if os.path.exists(args.traffic_json):
+    live = None
+    if pmc_enabled(args, world):
+        live = live_pmc(args, info, cfg, n)
+    traffic_source = None
+    if live and "hbm_bytes_per_launch" in live:
+        traffic, traffic_source = live["hbm_bytes_per_launch"], "pmc (this run: rocprofv3 --pmc children, pmc_live)"
+    elif os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
             if tkey in tj:
-                traffic = tj[tkey]["hbm_bytes_per_launch"]
+                traffic, traffic_source = tj[tkey]["hbm_bytes_per_launch"], "profiles/traffic.json (committed, same layout key)"
         except Exception:
             traffic = None
     issue = None  # the single-wave VALU issue ceiling, from the committed PMC passes
@@ -363,7 +372,7 @@ def main():
                                                    "waves_per_simd", "helper_wave", "wave_roles")},
                    "parallelism": f"dp{world} (skeleton shards, no data-path collective)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_key": tkey,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_key": tkey, "traffic_source": traffic_source,
                      "algorithmic_bytes_per_launch": alg_bytes, "kernel_ms": kernel_ms,
                      "note": "latency/VALU-bound serial chain; HBM fraction reported as requested (DESIGN.md §5)"},
         "valu": {"achieved": alg_flops / (kernel_ms * 1e-3) / 1e12, "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -377,6 +386,8 @@ def main():
         "pcie_inclusive": pcie,
         "parity": parity,
     }
+    if live is not None:
+        out["pmc_live"] = live
     if lib_multi is not None:
         out["library_multi"] = lib_multi
     if world > 1:
@@ -476,6 +487,90 @@ def layout_key(info: dict) -> str:
     return (f"K{info['lanes_per_skeleton']}_s{info['skeletons_per_block']}_i{info['checkpoint_interval']}"
             f"_st{info['heading_staging']}_pl{info['state_placement']}_w{info['waves_per_simd']}"
             + ("_h1" if info.get("helper_wave") else "") + ("_rw" if info.get("wave_roles") else ""))
+
+
+LAYOUT_FIELDS = ("lanes_per_skeleton", "skeletons_per_block", "checkpoint_interval", "heading_staging", "state_placement",
+                 "waves_per_simd", "helper_wave", "wave_roles")
+# one rocprofv3 --pmc pass each (FETCH_SIZE takes 3 of the 4 TCC counters, WRITE_SIZE 2)
+PMC_PASSES = (("FETCH_SIZE",), ("WRITE_SIZE",), ("SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_INSTS_VALU"))
+
+
+def pmc_enabled(args, world: int) -> bool:
+    """The live counter leg runs at N = 1 only, never inside a run that is itself profiled."""
+    import shutil
+    if args.pmc in ("off", "child") or world > 1:
+        return False
+    if args.pmc == "on":
+        return True
+    if any(k.startswith("ROCPROF") for k in os.environ) or "rocprof" in os.environ.get("LD_PRELOAD", ""):
+        return False
+    return shutil.which("rocprofv3") is not None
+
+
+def live_pmc(args, info: dict, cfg: int, n: int) -> dict:
+    """roofline.traffic and the VALU issue of THIS run's timed layout, measured rather than looked
+    up: after the timed region, rank 0 re-runs the same batch on the same layout in child
+    processes under `rocprofv3 --pmc` (one pass per counter group, each under its own KILL
+    time limit), and averages the solve kernel's timed dispatches.  HBM bytes per launch =
+    FETCH_SIZE x 2 + WRITE_SIZE (KB, gfx950 correction of MI355X_MICROARCH.md's HBM section;
+    calibrated for this kernel's loads in profiles/r03_fetch_calib.json).  constraint_mode
+    children autotune on their own (its frame-dependent layouts are not pinned by --layout); their
+    counters are used only when they land on the parent's layout."""
+    import csv
+    import glob
+    import subprocess
+    import tempfile
+    layout = ":".join(str(int(info[k])) for k in LAYOUT_FIELDS)
+    child = [sys.executable, os.path.abspath(__file__), "--config", str(cfg), "--skeletons", str(n), "--steps", "3",
+             "--warmup", "1", "--no-cpu-baseline", "--no-parity", "--pmc", "child"]
+    child += ["--constraint-mode"] if args.constraint_mode else ["--layout", layout]
+    if args.stabilization_passes:
+        child += ["--stabilization-passes", str(args.stabilization_passes)]
+    kern = "mbik_cmode_kernel" if args.constraint_mode else "mbik_solve_kernel"
+    tmp = tempfile.mkdtemp(prefix="mbik_pmc_", dir="/tmp")
+    env = dict(os.environ, TMPDIR="/tmp")
+    sums, keys = {}, set()
+    t0 = time.perf_counter()
+    for i, ctrs in enumerate(PMC_PASSES):
+        d = os.path.join(tmp, f"p{i}")
+        cmd = ["timeout", "-s", "KILL", "150", "rocprofv3", "--pmc", *ctrs, "-d", d, "-o", "run", "--output-format", "csv",
+               "--", *child]
+        r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True)
+        if r.returncode != 0:
+            return {"error": f"pass {' '.join(ctrs)}: exit {r.returncode}: {r.stderr.strip()[-300:]}"}
+        try:
+            keys.add(json.loads(r.stdout.strip().splitlines()[-1])["roofline"]["traffic_key"])
+        except Exception:  # noqa: BLE001
+            return {"error": f"pass {' '.join(ctrs)}: no bench line from the child"}
+        per = {}
+        for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            with open(path) as f:
+                for row in csv.DictReader(f):
+                    if kern in row["Kernel_Name"]:
+                        c = per.setdefault(int(row["Dispatch_Id"]), {})
+                        c[row["Counter_Name"]] = c.get(row["Counter_Name"], 0.0) + float(row["Counter_Value"])
+        timed = [per[k] for k in sorted(per)[-3:]]  # the child's three timed steps
+        if not timed:
+            return {"error": f"pass {' '.join(ctrs)}: no {kern} dispatches in the counter CSV"}
+        for ctr in ctrs:
+            sums[ctr] = sum(t.get(ctr, 0.0) for t in timed) / len(timed)
+    out = {"passes": [" ".join(c) for c in PMC_PASSES], "dispatches_averaged": 3, "child_layout_keys": sorted(keys),
+           "seconds": round(time.perf_counter() - t0, 1), "fetch_size_kb": sums["FETCH_SIZE"], "write_size_kb": sums["WRITE_SIZE"]}
+    tkey_parent = layout_key(info)
+    if not all(k.endswith(tkey_parent) for k in keys):
+        out["error"] = f"child layouts {sorted(keys)} differ from the timed layout {tkey_parent}"
+        return out
+    out["hbm_bytes_per_launch"] = sums["FETCH_SIZE"] * 1024 * 2 + sums["WRITE_SIZE"] * 1024
+    out["correction"] = "FETCH_SIZE x2 (gfx950) + WRITE_SIZE, KB x 1024"
+    w = max(sums["SQ_WAVES"], 1.0)
+    cyc = sums["SQ_WAVE_CYCLES"] * 4 / w  # SQ_WAVE_CYCLES counts 4-cycle units
+    valu = sums["SQ_INSTS_VALU"] / w
+    out["per_wave"] = {"waves": sums["SQ_WAVES"], "wave_cycles": cyc, "valu_insts": valu,
+                       "issue_frac": 4 * valu / cyc if cyc else None,
+                       "wait_any_frac": sums["SQ_WAIT_ANY"] / sums["SQ_WAVE_CYCLES"] if sums["SQ_WAVE_CYCLES"] else None,
+                       "note": "4 cycles per wave64 VALU instruction x VALU instructions / wave cycles; helper-wave "
+                               "layouts: the mean over the solving wave and its helper (the solving wave alone: `issue`)"}
+    return out
 
 
 def timed_gathers(pose_out, total: int, dist, sync, dev) -> dict:

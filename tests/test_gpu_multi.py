@@ -84,7 +84,7 @@ def test_bench_library_multi_on_one_box(mbik, torch_dev):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     cmd = [sys.executable, os.path.join(root, "bench.py"), "--config", "2", "--skeletons", "256", "--steps", "2",
-           "--warmup", "1", "--no-cpu-baseline", "--no-autotune", "--library-multi-devices", "0,0"]
+           "--warmup", "1", "--no-cpu-baseline", "--no-autotune", "--pmc", "off", "--library-multi-devices", "0,0"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=root)
     assert r.returncode == 0, r.stderr[-2000:]
     line = json.loads(r.stdout.strip().splitlines()[-1])

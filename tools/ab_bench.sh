@@ -1,4 +1,5 @@
 #!/bin/bash
+export MBIK_BENCH_PMC=${MBIK_BENCH_PMC:-off}  # timing-only bench runs: no live counter leg
 # A/B: bench C3/C4/C5 per variant (autotuned), interleaved twice
 mkdir -p gpurun_out
 for rep in 1 2; do

@@ -1,4 +1,5 @@
 #!/bin/bash
+export MBIK_BENCH_PMC=${MBIK_BENCH_PMC:-off}  # timing-only bench runs: no live counter leg
 # Same-box A/B of library variants on pinned layouts, interleaved REPS times (default 2):
 #   tools/ab_env.sh "<label>|<env assignments>|<lib .so or ->" ... -- <config>:<layout> [...]
 # e.g.  tools/ab_env.sh "rec|MBIK_RW_REC=1|-" "norec|MBIK_RW_REC=0|-" "base||build/diag/libmbik_abl_BASE.so" \

@@ -1,4 +1,5 @@
 #!/bin/bash
+export MBIK_BENCH_PMC=${MBIK_BENCH_PMC:-off}  # timing-only bench runs: no live counter leg
 # what do the helper-wave kernel's SGPR spills cost C2?  27 of the SGPRs it
 # keeps live are the topology tables' LDS offsets.  A timing-only build with the C2 plan's offsets
 # compiled in (tools/topo_const.py, solve_block.h MBIK_TOPO_CONST) frees them; same-box A/B of

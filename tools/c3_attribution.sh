@@ -1,4 +1,5 @@
 #!/bin/bash
+export MBIK_BENCH_PMC=${MBIK_BENCH_PMC:-off}  # timing-only bench runs: no live counter leg
 # where C3's waves wait (65,536 skeletons x 32 bones / 4 effectors, no
 # constraints), on the shipped classic layout and on the wave-roles layout, with the round-5
 # attribution tooling:

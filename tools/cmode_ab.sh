@@ -1,4 +1,5 @@
 #!/bin/bash
+export MBIK_BENCH_PMC=${MBIK_BENCH_PMC:-off}  # timing-only bench runs: no live counter leg
 # constraint_mode A/B: bench.py --constraint-mode on the given configs for each library, interleaved
 # twice (same box), each line with its 64-skeleton bitwise parity check:
 #   OUT=gpurun_out/<dir> CFGS="5 2" tools/cmode_ab.sh <lib> [...]     (<lib>: "new" = the in-tree build, or a .so path)

@@ -1,4 +1,5 @@
 #!/bin/bash
+export MBIK_BENCH_PMC=${MBIK_BENCH_PMC:-off}  # timing-only bench runs: no live counter leg
 # Same-box A/B of pinned launch layouts through bench.py, interleaved twice:
 #   tools/layout_ab.sh <config> <layout> [<layout> ...]     (layout = bench.py --layout)
 # Prints one line per run: layout, ms per step, bitwise parity of the bench's spot check.

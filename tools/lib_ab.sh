@@ -1,4 +1,5 @@
 #!/bin/bash
+export MBIK_BENCH_PMC=${MBIK_BENCH_PMC:-off}  # timing-only bench runs: no live counter leg
 # Same-box A/B of the in-tree library against build/abl/libmbik_abl_<tag>.so on pinned layouts,
 # interleaved twice:   [ABDIR=build/diag] [ENV_NEW="K=V"] tools/lib_ab.sh <tag> <config>:<layout> [...]
 # (build/abl is not pushed to GPU boxes: use ABDIR=build/diag there)

@@ -10,7 +10,7 @@ cd "$(dirname "$0")/.."
 ROOT=$PWD
 OUT=$ROOT/gpurun_out/$TAG
 mkdir -p $OUT
-export MBIK_LIB_OVERRIDE=$ROOT/build/abl/libmbik_replay.so
+export MBIK_LIB_OVERRIDE=${REPLAY_LIB:-$ROOT/build/diag/libmbik_replay.so}  # (OUT=build/diag/libmbik_replay.so tools/prof_build.sh REPLAY)
 timeout -k 10 120 python3 -u tools/replay_count.py $CASES > $OUT/plain.jsonl 2> $OUT/plain.err
 cat $OUT/plain.jsonl
 cd /tmp && export TMPDIR=/tmp
