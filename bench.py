@@ -21,6 +21,10 @@ other ranks wait on the host; it is reported under "library_multi", never as `va
 (--library-multi-devices 0,0 runs that measurement at N = 1 with the listed devices' plans:
 the one-GPU test of the same code.)
 
+At N = 1, after the timed region, rank 0 re-runs the timed layout in rocprofv3 --pmc child
+processes (FETCH_SIZE, WRITE_SIZE, SQ wave counters; `--pmc off` skips them): the line's
+roofline.traffic and pmc_live.per_wave come from this run, not from committed files.
+
 --dry-run exercises the launcher / rendezvous / sharding / timing plumbing on CPU (gloo,
 no GPU, no solve): the tests use it, its line says "dry_run": true and is never a result.
 """
@@ -43,6 +47,11 @@ VALU_PEAK_TFLOPS = 157.3  # MI355X FP32 vector peak (same guide)
 SKEL_PER_GPU = {2: 4096, 3: 65536, 4: 262144 // 8, 5: 16384}      # weak scaling
 SKEL_TOTAL = {2: 4096, 3: 65536, 4: 262144, 5: 16384}             # strong scaling (BASELINE configs)
 METRIC = "skeletons/sec to convergence (32-bone/4-eff, 16 iters) at 1/2/4/8 GPU; bone-quat max-err vs ref"
+
+
+def progress(msg: str) -> None:
+    """One line per phase on stderr: long runs (262,144-skeleton batches, autotune) keep writing."""
+    print(f"[bench {time.strftime('%H:%M:%S')} rank {os.environ.get('RANK', '0')}] {msg}", file=sys.stderr, flush=True)
 
 
 def parse():
@@ -176,8 +185,10 @@ def main():
 
     cfg = args.config
     total, first, n = batch_shard(args, world, rank)
+    progress(f"generate C{cfg}: {n} skeletons from {first}")
     wl = W.generate(cfg, n, first=first)
     flags = dict(constraint_mode=args.constraint_mode, stabilization_passes=args.stabilization_passes)
+    progress("plan")
     plan = Plan.from_workload(wl, device=local_rank, lanes=args.lanes, **flags)
     info = plan.info()
     pose_in = torch.from_numpy(wl.pose).to(dev)
@@ -202,8 +213,10 @@ def main():
     elif not args.no_autotune:
         # mbik_plan_autotune: times the candidate launch layouts on this very batch and keeps
         # the fastest (every layout computes identical bits); part of warmup, not timed.
+        progress("autotune")
         plan.autotune(pose_in.data_ptr(), targets.data_ptr(), pose_out.data_ptr(), 0, n, stream.cuda_stream)
         info = plan.info()
+    progress(f"warmup {args.warmup}, timed {args.steps}")
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
@@ -248,6 +261,7 @@ def main():
     # skeletons, so the largest per-skeleton offsets of the timed launch are checked too
     parity = None
     if not args.no_parity and rank == 0 and args.pmc != "child":
+        progress("parity")
         try:
             from oracle import pyoracle as po
             head = min(32, n)
@@ -282,6 +296,7 @@ def main():
             dist.barrier(group=host_group)
         if rank == 0:
             try:
+                progress("library_multi")
                 lib_multi = library_multi(cfg, [total // len(lm_devices)] * len(lm_devices), lm_devices, args, info, flags)
             except Exception as e:  # noqa: BLE001 -- measurement only: reported, never part of `value`
                 lib_multi = {"error": f"{type(e).__name__}: {e}"}
@@ -306,6 +321,7 @@ def main():
     tkey = key + "_" + layout_key(info)
     live = None
     if pmc_enabled(args, world):
+        progress("live counter passes")
         live = live_pmc(args, info, cfg, n)
     traffic_source = None
     if live and "hbm_bytes_per_launch" in live:
@@ -396,6 +412,7 @@ def main():
         out["rehearsal"] = f"all {world} ranks on cuda:{local_rank} (MBIK_BENCH_DEVICE): not a scaling measurement"
     if world == 1 and not args.no_cpu_baseline:
         try:
+            progress("cpu baseline")
             out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds, **flags)
         except Exception as e:
             out["cpu_baseline"] = {"error": str(e)}
