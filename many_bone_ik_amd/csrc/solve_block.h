@@ -11,6 +11,14 @@ namespace {
 #ifndef MBIK_WAVES_PER_EU
 #define MBIK_WAVES_PER_EU 1
 #endif
+// Wave roles: while a cooperative row's first wave runs a bone-step, every other wave of its
+// block waits at the barrier, so that wave alone is the block's critical path.  It raises its
+// issue priority for the step (s_setprio) above the other block's wave on its SIMD, which has
+// slack then.  C4 -2.6 %, C5 within noise, for priorities 1 to 3 alike (same box, interleaved:
+// profiles/r06_rw_priority_ab.txt).  0 = off.
+#ifndef MBIK_RW_PRIO
+#define MBIK_RW_PRIO 1
+#endif
 // The solve of one block (blk = the plan-local block index after the XCD remap).
 // Wave-uniform bone-step count of schedule row r: the longest segment among its tasks (the
 // helper and the solving wave walk the same (row, step) sequence).  For a whole-plan solve it
@@ -314,9 +322,11 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 						MBIK_PROF_T(c2);
 						MBIK_PROF_ADD(21, c1, c2);
 						if (leader) {
+							if constexpr (MBIK_RW_PRIO > 0) __builtin_amdgcn_s_setprio(MBIK_RW_PRIO);
 							if (step)
 								bone_step<false, true, TA, false, false, PM, HOIST, true>(t, seg, k0 + q, 0, 1, coop ? 1 : 0, s, L, G, TG, ST,
 										SF, HS, OE, MS, prev_dev, pre, hoist, rec, rcnt, q + 1, nullptr, xw MBIK_PROF_ARG);
+							if constexpr (MBIK_RW_PRIO > 0) __builtin_amdgcn_s_setprio(0);
 						} else if (producer && act && k0 + q + 1 < k1) {
 							// the next step's record, stored once the first wave has read this step's
 							const RwRec next = rw_record(t, k0 + q + 1, L, G);

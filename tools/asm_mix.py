@@ -1,10 +1,10 @@
-"""Static instruction mix of one kernel in build/asm/solve.s (run tools/asm_stats.sh first).
-    python tools/asm_mix.py [kernel-substring]"""
+"""Static instruction mix of one kernel in build/asm/<tu>.s (run tools/asm_stats.sh first).
+    python tools/asm_mix.py [kernel-substring] [build/asm/<tu>.s]"""
 import collections
 import sys
 
 name = sys.argv[1] if len(sys.argv) > 1 else "mbik_solve_kernelILb0E"
-s = open("build/asm/solve.s").read().split("\n")
+s = open(sys.argv[2] if len(sys.argv) > 2 else "build/asm/k_solve_rw.s").read().split("\n")
 start = next(i for i, l in enumerate(s) if name in l and l.split(":")[0].endswith(l.split(":")[0]) and l.startswith("_Z"))
 end = next(i for i in range(start, len(s)) if s[i].strip().startswith("s_endpgm") or s[i].startswith(".Lfunc_end"))
 c = collections.Counter()
