@@ -11,11 +11,13 @@ namespace {
 #ifndef MBIK_WAVES_PER_EU
 #define MBIK_WAVES_PER_EU 1
 #endif
-// Wave roles: while a cooperative row's first wave runs a bone-step, every other wave of its
-// block waits at the barrier, so that wave alone is the block's critical path.  It raises its
-// issue priority for the step (s_setprio) above the other block's wave on its SIMD, which has
-// slack then.  C4 -2.6 %, C5 within noise, for priorities 1 to 3 alike (same box, interleaved:
-// profiles/r06_rw_priority_ab.txt).  0 = off.
+// Wave roles: a cooperative row is block-synchronous (two barriers per bone-step), and while its
+// first wave runs a step the rest of the block waits, so its waves are their block's critical
+// path; a wave of the other block resident on the SIMD, in a row without barriers, has slack.
+// The row's waves run it at raised issue priority (s_setprio; arbitration is priority, then
+// age).  C4 -4.3 % against none (only the stepping wave raised: -2.6 %; the walks and the step
+// raised to 2: -1.4 %), C5 within noise (same box, interleaved: profiles/r06_rw_priority_ab.txt).
+// 0 = off.
 #ifndef MBIK_RW_PRIO
 #define MBIK_RW_PRIO 1
 #endif
@@ -312,6 +314,7 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 					// (MBIK_PROF, wave roles: 18 packed / plain rows, 19 coop_walk, 21 waiting at the
 					// cooperative rows' barriers, 22 the steps run after them, 23 cooperative rows)
 					MBIK_PROF_T(cr0);
+					if constexpr (MBIK_RW_PRIO > 0) __builtin_amdgcn_s_setprio(MBIK_RW_PRIO);
 					for (int q = 0; q < nq; q++) {
 						const bool step = act && k0 + q < k1;
 						MBIK_PROF_T(c0);
@@ -322,11 +325,9 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 						MBIK_PROF_T(c2);
 						MBIK_PROF_ADD(21, c1, c2);
 						if (leader) {
-							if constexpr (MBIK_RW_PRIO > 0) __builtin_amdgcn_s_setprio(MBIK_RW_PRIO);
 							if (step)
 								bone_step<false, true, TA, false, false, PM, HOIST, true>(t, seg, k0 + q, 0, 1, coop ? 1 : 0, s, L, G, TG, ST,
 										SF, HS, OE, MS, prev_dev, pre, hoist, rec, rcnt, q + 1, nullptr, xw MBIK_PROF_ARG);
-							if constexpr (MBIK_RW_PRIO > 0) __builtin_amdgcn_s_setprio(0);
 						} else if (producer && act && k0 + q + 1 < k1) {
 							// the next step's record, stored once the first wave has read this step's
 							const RwRec next = rw_record(t, k0 + q + 1, L, G);
@@ -339,6 +340,7 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 						MBIK_PROF_T(c4);
 						MBIK_PROF_ADD(21, c3, c4);
 					}
+					if constexpr (MBIK_RW_PRIO > 0) __builtin_amdgcn_s_setprio(0);
 					MBIK_PROF_T(cr1);
 					MBIK_PROF_ADD(23, cr0, cr1);
 					r++;
