@@ -705,10 +705,20 @@ void build_schedule(HostPlan &p, int32_t lanes, int64_t nlaunch, int32_t spw_ove
 			std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return seg_cost(a) > seg_cost(b); });
 			std::vector<std::vector<int>> per(K);
 			std::vector<int64_t> load(K, 0);
+			// (eight wave roles put roles 2i and 2i + 1 on one SIMD, MBIK_RW_PERM: the SIMDs' loads
+			// are balanced first, then the two roles' on each)
+			const bool pair = MBIK_RW_PERM && p.wave_roles && !p.constraint_mode && K == 8;
 			for (int sg : order) {
 				int i = -1;
-				for (int q = 0; q < K; q++)
-					if ((!p.constraint_mode || per[q].size() < 4) && (i < 0 || load[q] < load[i])) i = q;
+				if (pair) {
+					int sm = 0;
+					for (int q = 1; q < K / 2; q++)
+						if (load[2 * q] + load[2 * q + 1] < load[2 * sm] + load[2 * sm + 1]) sm = q;
+					i = load[2 * sm + 1] < load[2 * sm] ? 2 * sm + 1 : 2 * sm;
+				} else {
+					for (int q = 0; q < K; q++)
+						if ((!p.constraint_mode || per[q].size() < 4) && (i < 0 || load[q] < load[i])) i = q;
+				}
 				per[i].push_back(sg);
 				load[i] += seg_cost(sg);
 			}

@@ -54,6 +54,16 @@ constexpr int CFC_NCP = 13, CFC_C1XC2 = 16, CFC_A1 = 19, CFC_A2 = 22, CFC_B1 = 2
 // Per-skeleton double fields of one constraint slot, per cone: radius cosine, tangent radius cosine.
 constexpr int CD_PER_CONE = 2;
 
+// Wave roles with eight roles: a block's waves w and w + 4 share SIMD w % 4.  Roles 2i and
+// 2i + 1 -- a two-wave cooperative group's stepping wave and its partner -- go to waves i and
+// i + 4 (solve_block.h), so that the groups' stepping waves run on four different SIMDs instead
+// of two (C5 -1.9 %), and a packed level balances the SIMDs' estimated work before the two
+// roles' within each SIMD (build_schedule; C5 -2.5 %).  Same box, interleaved:
+// profiles/r06_rw_priority_ab.txt.  0 = roles in wave order, per-role packing.
+#ifndef MBIK_RW_PERM
+#define MBIK_RW_PERM 1
+#endif
+
 struct SchedTask {
 	int32_t seg;  // -1 idle
 	int32_t j;    // index of this lane inside the segment's lane group

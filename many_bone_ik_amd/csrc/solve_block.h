@@ -21,13 +21,6 @@ namespace {
 #ifndef MBIK_RW_PRIO
 #define MBIK_RW_PRIO 1
 #endif
-// Eight roles (two waves per SIMD from one block: waves w and w + 4 share SIMD w % 4): a
-// two-wave cooperative group's stepping wave and its partner (roles 2i, 2i + 1) go to waves i
-// and i + 4, so that the groups' stepping waves run on four different SIMDs instead of two.
-// C5 -1.9 % (same box, interleaved: profiles/r06_rw_priority_ab.txt).  0 = roles in wave order.
-#ifndef MBIK_RW_PERM
-#define MBIK_RW_PERM 1
-#endif
 // The solve of one block (blk = the plan-local block index after the XCD remap).
 // Wave-uniform bone-step count of schedule row r: the longest segment among its tasks (the
 // helper and the solving wave walk the same (row, step) sequence).  For a whole-plan solve it
@@ -88,7 +81,7 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 		t.D = dl; t.CF = cl; t.CD = xl; t.N = 1;
 	}
 	const int g = RW ? lane : lane >> t.log2K;
-	// (MBIK_RW_PERM: the role of each wave)
+	// (MBIK_RW_PERM, plan.h: the role of each wave)
 	const int role = RW ? ((RW == 8 && MBIK_RW_PERM) ? 2 * (wave & 3) + (wave >> 2) : wave) : lane & (t.K - 1);
 	const int local = blk * t.spw + g;
 	const bool valid = g < t.spw && local < count;
