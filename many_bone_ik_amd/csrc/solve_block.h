@@ -21,6 +21,12 @@ namespace {
 #ifndef MBIK_RW_PRIO
 #define MBIK_RW_PRIO 1
 #endif
+// Eight roles (MBIK_RW_PERM): a group of four or eight waves takes its record producer from
+// role 2, whose wave runs on another SIMD than the stepping wave's (role 1 shares it).  C5
+// -0.2 %, four of four interleaved reps (profiles/r06_rw_priority_ab.txt).
+#ifndef MBIK_RW_PROD2
+#define MBIK_RW_PROD2 1
+#endif
 // The solve of one block (blk = the plan-local block index after the XCD remap).
 // Wave-uniform bone-step count of schedule row r: the longest segment among its tasks (the
 // helper and the solving wave walk the same (row, step) sequence).  For a whole-plan solve it
@@ -309,7 +315,7 @@ __device__ __forceinline__ void solve_block(DevPlan &t, int blk, int first, int 
 					float4 *rec = rec_on ? xr4 + grp * (mbik::kRwRecF4 * 64) + lane : nullptr;
 					int *rcnt = rec_on ? rw_cnt + grp : nullptr;
 					const bool leader = ty == 0;
-					const bool producer = rec_on && ty == 1;
+					const bool producer = rec_on && ty == ((MBIK_RW_PROD2 && RW == 8 && MBIK_RW_PERM && task.z >= 4) ? 2 : 1);
 					if (leader && rec_on) *rcnt = 0; // (read only after the row's first barrier)
 					if (producer && act && k0 < k1) rw_record_store(rec, rw_record(t, k0, L, G));
 					// (MBIK_PROF, wave roles: 18 packed / plain rows, 19 coop_walk, 21 waiting at the
