@@ -533,9 +533,7 @@ def live_pmc(args, info: dict, cfg: int, n: int) -> dict:
     calibrated for this kernel's loads in profiles/r03_fetch_calib.json).  constraint_mode
     children autotune on their own (its frame-dependent layouts are not pinned by --layout); their
     counters are used only when they land on the parent's layout."""
-    import csv
-    import glob
-    import subprocess
+    import shutil
     import tempfile
     layout = ":".join(str(int(info[k])) for k in LAYOUT_FIELDS)
     child = [sys.executable, os.path.abspath(__file__), "--config", str(cfg), "--skeletons", str(n), "--steps", "3",
@@ -545,6 +543,16 @@ def live_pmc(args, info: dict, cfg: int, n: int) -> dict:
         child += ["--stabilization-passes", str(args.stabilization_passes)]
     kern = "mbik_cmode_kernel" if args.constraint_mode else "mbik_solve_kernel"
     tmp = tempfile.mkdtemp(prefix="mbik_pmc_", dir="/tmp")
+    try:
+        return _live_pmc_passes(child, kern, tmp, info)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
+def _live_pmc_passes(child, kern: str, tmp: str, info: dict) -> dict:
+    import csv
+    import glob
+    import subprocess
     env = dict(os.environ, TMPDIR="/tmp")
     sums, keys = {}, set()
     t0 = time.perf_counter()
