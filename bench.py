@@ -359,6 +359,16 @@ def main():
                                     if info.get("helper_wave") else "")}
         except Exception:
             issue = None
+    if issue is not None:
+        issue["source"] = "profiles/valu_mix.json (committed, same layout key)"
+    pw = (live or {}).get("per_wave") if live and "hbm_bytes_per_launch" in live else None
+    if pw and pw.get("issue_frac") and not info.get("helper_wave"):
+        # one kind of wave per block: this run's own counters replace the committed mix
+        issue = {"bound": "valu_issue_1wave", "achieved_cycles_per_wave": 4 * pw["valu_insts"],
+                 "valu_insts_per_wave": pw["valu_insts"], "wave_cycles": pw["wave_cycles"], "frac": pw["issue_frac"],
+                 "source": "pmc_live (this run)",
+                 "note": "4 cycles per wave64 VALU instruction x VALU instructions / wave cycles; the ceiling this "
+                         "latency-bound chain runs against"}
     out = {
         "metric": METRIC,
         "value": value,

@@ -43,3 +43,15 @@ def test_bench_pmc_off_reports_its_source():
     assert "pmc_live" not in line
     rf = line["roofline"]
     assert rf["traffic"] is None or rf["traffic_source"].startswith("profiles/traffic.json")
+
+
+@pytest.mark.skipif(shutil.which("rocprofv3") is None, reason="rocprofv3 not on PATH")
+def test_bench_issue_is_measured_for_one_wave_layouts():
+    """A layout with one kind of wave per block takes `issue` from the run's own counters; the
+    helper-wave layout keeps the committed replay figure of its solving wave (and says so)."""
+    line = run_bench("--layout", "4:16:1:1:0:1:0", "--pmc", "on")
+    assert "error" not in line["pmc_live"], line["pmc_live"]
+    assert line["issue"]["source"] == "pmc_live (this run)"
+    assert line["issue"]["frac"] == line["pmc_live"]["per_wave"]["issue_frac"]
+    helper = run_bench("--layout", "4:16:1:1:0:1:1", "--pmc", "on")
+    assert helper["issue"] is None or helper["issue"]["source"].startswith("profiles/valu_mix.json")
