@@ -559,8 +559,25 @@ def live_pmc(args, info: dict, cfg: int, n: int) -> dict:
         shutil.rmtree(tmp, ignore_errors=True)
 
 
-def _live_pmc_passes(child, kern: str, tmp: str, info: dict) -> dict:
+def counter_means(paths, kern: str, ctrs, last: int = 3):
+    """Per counter, the mean over the last `last` dispatches of kernels whose name contains
+    `kern` in rocprofv3 counter_collection CSVs (a dispatch's rows are summed: one per counter
+    instance); None if no such dispatch."""
     import csv
+    per = {}
+    for path in paths:
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                if kern in row["Kernel_Name"]:
+                    c = per.setdefault(int(row["Dispatch_Id"]), {})
+                    c[row["Counter_Name"]] = c.get(row["Counter_Name"], 0.0) + float(row["Counter_Value"])
+    timed = [per[k] for k in sorted(per)[-last:]]
+    if not timed:
+        return None
+    return {ctr: sum(t.get(ctr, 0.0) for t in timed) / len(timed) for ctr in ctrs}
+
+
+def _live_pmc_passes(child, kern: str, tmp: str, info: dict) -> dict:
     import glob
     import subprocess
     env = dict(os.environ, TMPDIR="/tmp")
@@ -577,18 +594,10 @@ def _live_pmc_passes(child, kern: str, tmp: str, info: dict) -> dict:
             keys.add(json.loads(r.stdout.strip().splitlines()[-1])["roofline"]["traffic_key"])
         except Exception:  # noqa: BLE001
             return {"error": f"pass {' '.join(ctrs)}: no bench line from the child"}
-        per = {}
-        for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
-            with open(path) as f:
-                for row in csv.DictReader(f):
-                    if kern in row["Kernel_Name"]:
-                        c = per.setdefault(int(row["Dispatch_Id"]), {})
-                        c[row["Counter_Name"]] = c.get(row["Counter_Name"], 0.0) + float(row["Counter_Value"])
-        timed = [per[k] for k in sorted(per)[-3:]]  # the child's three timed steps
-        if not timed:
+        mean = counter_means(glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True), kern, ctrs)
+        if mean is None:
             return {"error": f"pass {' '.join(ctrs)}: no {kern} dispatches in the counter CSV"}
-        for ctr in ctrs:
-            sums[ctr] = sum(t.get(ctr, 0.0) for t in timed) / len(timed)
+        sums.update(mean)
     out = {"passes": [" ".join(c) for c in PMC_PASSES], "dispatches_averaged": 3, "child_layout_keys": sorted(keys),
            "seconds": round(time.perf_counter() - t0, 1), "fetch_size_kb": sums["FETCH_SIZE"], "write_size_kb": sums["WRITE_SIZE"]}
     tkey_parent = layout_key(info)
