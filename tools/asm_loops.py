@@ -1,6 +1,6 @@
 """Static per-loop instruction counts of one kernel in an asm listing (tools/asm_stats.sh output,
 or a -gline-tables-only listing for per-source-line attribution).
-    python tools/asm_loops.py build/asm/solve_g.s kernel_substring [loop_label_for_line_detail]"""
+    python tools/asm_loops.py build/asm/<tu>.s kernel_substring [loop_label_for_line_detail]   (tools/asm_stats.sh -gline-tables-only)"""
 import collections
 import re
 import sys
