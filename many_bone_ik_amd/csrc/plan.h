@@ -54,7 +54,8 @@ constexpr int CFC_NCP = 13, CFC_C1XC2 = 16, CFC_A1 = 19, CFC_A2 = 22, CFC_B1 = 2
 // Per-skeleton double fields of one constraint slot, per cone: radius cosine, tangent radius cosine.
 constexpr int CD_PER_CONE = 2;
 
-// Wave roles with eight roles: a block's waves w and w + 4 share SIMD w % 4.  Roles 2i and
+// Wave roles with eight roles: a block's waves w and w + 4 share a SIMD, and waves 0-3 sit on
+// four different SIMDs (measured: tools/hwid_probe.hip, profiles/r06_wave_placement_probe_*).  Roles 2i and
 // 2i + 1 -- a two-wave cooperative group's stepping wave and its partner -- go to waves i and
 // i + 4 (solve_block.h), so that the groups' stepping waves run on four different SIMDs instead
 // of two (C5 -1.9 %), and a packed level balances the SIMDs' estimated work before the two
